@@ -1,0 +1,194 @@
+#!/usr/bin/env python3
+"""Headline benchmark: images/s of DeiT-base/16-224 at bs=512 per GPU, bf16, on N MI355X GPUs.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]             (N=1)
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+A step = one forward of the whole batch (patchify -> patch GEMM -> 12 x [LN, QKV GEMM,
+attention, out-proj GEMM + residual, LN, FC1 GEMM + GELU, FC2 GEMM + residual] -> head) through
+libevt_hip.so, plus, for N > 1, the RCCL all-gather of every rank's logits (the only exchange step
+of the path: images are independent). Inputs are synthetic N(0,1) images already
+resident in HBM; weights are the deterministic random init (no checkpoints exist offline).
+Scaling is weak: each rank runs its own bs=512 batch.
+
+Extra objects on the JSON line:
+  roofline      the dominant kernel (FC1 GEMM, M = 512*197, K = 768, N = 3072, 31.8% of the
+                model's FLOPs; ties with FC2) timed with HIP events on the stream it runs on;
+                achieved = 2*M*N*K / avg launch time vs the 2.5 PF dense bf16 MFMA peak.
+  cpu_baseline  the numpy fp32 restatement of the reference forward (oracle/, "port": TF is not
+                installed anywhere), DeiT-base bs=1 forwards for ~15 s on the host BLAS threads.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+PEAK_BF16_TFLOPS = 2516.6   # MI355X dense bf16 MFMA (spec; MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3     # MI355X fp32 matrix (spec)
+METRIC = "images/sec DeiT-base/16-224 bs=512 @1/2/4/8 GPU; % bf16 MFMA roofline"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=512, help="images per GPU")
+    ap.add_argument("--model", default="deit_base", choices=["deit_base", "deit_small", "deit_tiny"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--no-probe", action="store_true", help="skip the per-kernel probe")
+    return ap.parse_args()
+
+
+def kernel_probe(dtype: str, M: int, K: int, N: int, iters: int = 20) -> float:
+    """Average duration (s) of one FC1-shaped GEMM launch (bias + GELU epilogue), HIP events."""
+    from edgevisiontransformer_amd import _lib
+    lib = _lib.load_library()
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    dev = torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator(device=dev).manual_seed(123)
+    A = torch.randn((M, K), generator=g, device=dev).to(tdt)
+    W = torch.randn((K, N), generator=g, device=dev) / K ** 0.5
+    kpad, npad = (K + 63) // 64 * 64, (N + 127) // 128 * 128
+    wp = torch.empty((npad, kpad), dtype=tdt, device=dev)
+    bias = torch.zeros(npad, device=dev)
+    C = torch.empty((M, N), dtype=tdt, device=dev)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    _lib.check(lib.evt_pack_weight(_lib.DTYPE[dtype], P(W), K, N, P(wp), kpad, npad, s))
+
+    def launch():
+        _lib.check(lib.evt_dense(_lib.DTYPE[dtype], _lib.EPI_BIAS | _lib.EPI_GELU, P(A), K, P(wp),
+                                 kpad, npad, P(C), N, M, N, P(bias), ctypes.c_void_p(0), 0,
+                                 ctypes.c_void_p(0), 0, 0, s))
+    for _ in range(3):
+        launch()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(iters):
+        launch()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / 1e3 / iters
+
+
+def cpu_baseline(model_name: str, budget_s: float) -> dict:
+    from oracle.vit_ref import vit_forward
+    from edgevisiontransformer_amd.weights import make_images, make_vit_params
+    from edgevisiontransformer_amd.modeling.models.vit import _cfg_for as cfg_for
+    cfg = cfg_for(model_name)
+    params = make_vit_params(cfg, seed=0)
+    p32 = {k: v.astype(np.float32) for k, v in params.items()}
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:
+        cores = os.cpu_count() or 1
+    img = make_images(1, seed=99)
+    vit_forward(p32, cfg, img, dtype=np.float32)  # warm BLAS
+    n, t0 = 0, time.perf_counter()
+    while True:
+        vit_forward(p32, cfg, img, dtype=np.float32)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 200:
+            break
+    return {"value": n / el, "unit": "images/s", "cores": int(cores), "kind": "port",
+            "sample": f"{n} x {model_name} bs=1 forwards of the numpy fp32 restatement "
+                      f"(oracle/vit_ref.py) in {el:.1f} s; reference TF-CPU path not installable"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from edgevisiontransformer_amd.modeling.models import vit as vitmod
+    model = vitmod.build_named(args.model, dtype=args.dtype, seed=0, max_batch=args.batch)
+    B = args.batch
+    g = torch.Generator(device="cuda").manual_seed(1000 + rank)
+    img = torch.randn((B, 3, 224, 224), generator=g, device="cuda", dtype=torch.float32)
+    logits = torch.empty((B, model.num_classes), device="cuda", dtype=torch.float32)
+    gathered = torch.empty((world * B, model.num_classes), device="cuda") if world > 1 else None
+
+    def step():
+        model.forward_into(img, logits)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, logits)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ok = bool(torch.isfinite(logits).all().item())
+
+    gflop_img = model.cfg.gflop_per_image()
+    imgs_per_s = world * B * args.steps / el
+    peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
+    roof = None
+    if rank == 0 and not args.no_probe:
+        M, K, N = B * model.cfg.tokens, model.cfg.dim, model.cfg.ffn[0]
+        t_k = kernel_probe(args.dtype, M, K, N)
+        ach = 2.0 * M * N * K / t_k / 1e12
+        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(ach / peak, 4), "traffic": None,
+                "kernel": f"gemm_nt_kernel<{args.dtype}, bias+gelu> FC1 M={M} K={K} N={N}",
+                "avg_launch_us": round(t_k * 1e6, 1)}
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(args.model, args.cpu_seconds)
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(imgs_per_s, 2), "unit": "images/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic N(0,1) NCHW images resident in HBM; deterministic random-init weights",
+            "config": {"workload": f"{args.model}/16-224 forward, bs={B} per GPU, {args.dtype}",
+                       "model": args.model, "global_batch": world * B, "per_gpu_batch": B,
+                       "seq_len": model.cfg.tokens, "parallelism": f"dp{world} (batch shard, "
+                       "RCCL all-gather of logits)" if world > 1 else "dp1"},
+            "model_roofline": {"achieved_tflops": round(imgs_per_s * gflop_img / world / 1e3, 2),
+                               "peak": peak, "frac": round(imgs_per_s * gflop_img / world / 1e3
+                                                           / peak, 4),
+                               "gflop_per_image": round(gflop_img, 3)},
+            "roofline": roof, "cpu_baseline": cpu, "logits_finite": ok,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,110 @@
+"""ctypes binding of libevt_hip.so (C ABI in include/evt.h).
+
+There is deliberately no CPU or PyTorch fallback: if the HIP library is missing or the device is
+not a gfx950 GPU, every call raises. torch is imported first so that the HIP runtime torch ships
+(SONAME libamdhip64.so.7) is the one the library binds to: one runtime per process, and torch
+device pointers / streams are valid handles for the library.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must be loaded before the HIP library, see module doc)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("EVT_LIB", os.path.join(_HERE, "libevt_hip.so"))
+
+EVT_OK = 0
+EVT_EINVAL = -22
+EVT_ENOMEM = -12
+EVT_EHIP = -5
+EVT_ENODEV = -19
+DTYPE = {"f32": 0, "fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1}
+
+# GEMM epilogue flags (csrc/evt_internal.h)
+EPI_BIAS, EPI_GELU, EPI_RESID, EPI_POS, EPI_OUT_F32 = 1, 2, 4, 8, 16
+
+
+class EvtError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"evt error {code}: {msg}")
+        self.code = code
+
+
+class evt_vit_desc(ctypes.Structure):
+    _fields_ = [("image_size", ctypes.c_int32), ("patch_size", ctypes.c_int32),
+                ("in_chans", ctypes.c_int32), ("num_classes", ctypes.c_int32),
+                ("dim", ctypes.c_int32), ("depth", ctypes.c_int32), ("mlp_dim", ctypes.c_int32),
+                ("heads", ctypes.POINTER(ctypes.c_int32)),
+                ("head_dim", ctypes.POINTER(ctypes.c_int32)),
+                ("ffn", ctypes.POINTER(ctypes.c_int32)),
+                ("dtype", ctypes.c_int32), ("max_batch", ctypes.c_int32)]
+
+
+# name -> (restype, argtypes); this is the full symbol list of include/evt.h
+_P, _I, _I64, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
+SIGNATURES = {
+    "evt_init": (_I, [_I]),
+    "evt_last_error": (ctypes.c_char_p, []),
+    "evt_vit_num_weights": (_I, [ctypes.POINTER(evt_vit_desc)]),
+    "evt_vit_create": (_I, [ctypes.POINTER(evt_vit_desc), ctypes.POINTER(_P), _I, _P,
+                            ctypes.POINTER(_P)]),
+    "evt_vit_forward": (_I, [_P, _P, _I, _P, _P]),
+    "evt_query_workspace": (_I, [ctypes.POINTER(evt_vit_desc), _I, ctypes.POINTER(ctypes.c_size_t)]),
+    "evt_model_destroy": (_I, [_P]),
+    "evt_pack_weight": (_I, [_I, _P, _I, _I, _P, _I, _I, _P]),
+    "evt_dense": (_I, [_I, _I, _P, _I64, _P, _I, _I, _P, _I64, _I, _I, _P, _P, _I64, _P, _I64, _I,
+                       _P]),
+    "evt_attention": (_I, [_I, _P, _I64, _P, _I64, _I, _I, _I, _F, _P]),
+    "evt_layernorm": (_I, [_I, _P, _I64, _P, _I64, _P, _P, _I, _I, _F, _P]),
+    "evt_patchify": (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P]),
+}
+
+_lib = None
+_lock = threading.Lock()
+_initialized_devices = set()
+
+
+def load_library() -> ctypes.CDLL:
+    """Load (once) and type the library; raises if it is not built."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"{LIB_PATH} not found: build it with `python -m edgevisiontransformer_amd.build`"
+                    " (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+            lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def last_error() -> str:
+    return load_library().evt_last_error().decode(errors="replace")
+
+
+def check(rc: int) -> None:
+    if rc != EVT_OK:
+        raise EvtError(rc, last_error())
+
+
+def ensure_device(device_index: int) -> None:
+    """evt_init once per device: requires a visible gfx950 GPU (fails loudly otherwise)."""
+    if device_index in _initialized_devices:
+        return
+    if not torch.cuda.is_available():
+        raise RuntimeError("edgevisiontransformer_amd needs a ROCm GPU (MI355X / gfx950); "
+                           "torch.cuda.is_available() is False and there is no CPU fallback")
+    lib = load_library()
+    check(lib.evt_init(device_index))
+    _initialized_devices.add(device_index)
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,65 @@
+"""Build libevt_hip.so (gfx950) in-tree with hipcc; no torch extension machinery involved.
+
+`python -m edgevisiontransformer_amd.build` or `__graft_entry__.build()`. Objects are compiled in
+parallel; the link is skipped when every source is older than the library.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libevt_hip.so")
+OBJ = os.path.join(HERE, "build_obj")
+SOURCES = ["gemm.hip", "attention.hip", "norm.hip", "capi.cpp"]
+HEADERS = ["common.h", "evt_internal.h", os.path.join("..", "..", "include", "evt.h")]
+ARCH = os.environ.get("EVT_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.isabs(c) and os.path.exists(c) or not os.path.isabs(c)):
+            return c
+    return "hipcc"
+
+
+def _mtime(p: str) -> float:
+    return os.path.getmtime(p) if os.path.exists(p) else 0.0
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    hdr_t = max(_mtime(os.path.join(CSRC, h)) for h in HEADERS)
+    jobs = []
+    objs = []
+    for src in SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(OBJ, src + ".o")
+        objs.append(o)
+        if force or _mtime(o) < max(_mtime(s), hdr_t):
+            cmd = [_hipcc(), *FLAGS, "-c", s, "-o", o]
+            if src.endswith(".cpp"):
+                cmd = [_hipcc(), "-O3", "-std=c++17", "-fPIC", "-c", s, "-o", o]
+            jobs.append(cmd)
+
+    def run(cmd):
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        if verbose:
+            print(" ".join(cmd))
+        return r
+
+    with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
+        list(ex.map(run, jobs))
+    if force or jobs or _mtime(LIB) < max(_mtime(o) for o in objs):
+        run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB])
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

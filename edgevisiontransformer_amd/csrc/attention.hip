@@ -1,0 +1,278 @@
+// Fused multi-head self-attention for the ViT encoder on gfx950.
+//
+// Replaces reference `modeling/layers/attention.py:20-34`: the (qkv h d) split, q.k^T * h_k^-0.5,
+// tf.nn.softmax, attn.v and the 'b h n d -> b n (h d)' rearrange, without materialising the
+// [B, h, N, N] score tensor (954 MB per layer at DeiT-base bs512 in fp32).
+//
+// One workgroup per (image, head); 4 waves. K and V of the head (N <= 256 rows x 64) are staged
+// once into LDS with global_load_lds straight from the QKV GEMM output (token rows, columns
+// (qkv h d), so no re-layout kernel exists), rows past N clamped (their scores are masked to -inf
+// and their P is exactly 0). Each wave then walks 16-query tiles:
+//
+//   S^T = K . Q^T      (MFMA A = K rows from LDS, B = Q rows straight from global)
+//   exact softmax      (the key axis lives in registers + 4 lane groups: 2 shuffles per reduction)
+//   O^T = V^T . P^T    (A = V^T via ds_read_b64_tr_b16 transposed LDS reads; B = P^T is the S^T
+//                       accumulator itself, converted to bf16 in place: no LDS round trip)
+//
+// Computing the transposed products puts one query per lane column, so the row max / row sum and
+// the final 1/l scaling are lane-local, and each lane stores 4 consecutive head features.
+// LDS images use the swizzle chunk ^ (row & 7) (bf16, 128-B rows) / chunk ^ (row & 15) (fp32,
+// 256-B rows), applied on the glds source address and on every read: conflict-free for both the
+// row reads and the transposed reads (checked with the bank model of the CDNA4 guide).
+//
+// The fp32 variant (exact v_mfma_f32_16x16x4_f32, for the 1e-3 parity path) uses the same
+// structure; its V^T operand is a plain ds_read_b32 per MFMA.
+#include "common.h"
+#include "evt_internal.h"
+
+namespace evt {
+
+namespace {
+
+template <int NKT>  // 16-key tiles (keys padded to NKT*16, multiple of 32)
+__global__ __launch_bounds__(256) void attn_bf16_kernel(AttnParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NP = NKT * 16;
+  constexpr int ROWB = 128;  // 64 bf16
+  EVT_LDS char* Ks = (EVT_LDS char*)smem;
+  EVT_LDS char* Vs = Ks + NP * ROWB;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x / p.H, h = blockIdx.x - b * p.H;
+  const bf16* qkv = (const bf16*)p.qkv + (int64_t)b * p.N * p.ldq;
+
+  // ---- stage K, V (8 rows of 128 B per wave-instruction) ----
+  {
+    const int srow = lane >> 3, sslot = lane & 7;
+    for (int i = wave; i < NP / 8; i += 4) {
+      const int row = i * 8 + srow;
+      const int gr = min(row, p.N - 1);
+      const bf16* rp = qkv + (int64_t)gr * p.ldq + ((sslot ^ srow) * 8);
+      glds16(rp + (p.H + h) * 64, Ks + i * 8 * ROWB);
+      glds16(rp + (2 * p.H + h) * 64, Vs + i * 8 * ROWB);
+    }
+    wait_vmcnt0();
+    __syncthreads();
+  }
+
+  const int g = lane >> 4, c16 = lane & 15, sw = lane & 7;
+  const int nqt = (p.N + 15) >> 4;
+  for (int qt = wave; qt < nqt; qt += 4) {
+    const int qi = min(qt * 16 + c16, p.N - 1);
+    const bf16* qrow = qkv + (int64_t)qi * p.ldq + h * 64;
+    const u32x4 qf0 = *(const u32x4*)(qrow + 8 * g);
+    const u32x4 qf1 = *(const u32x4*)(qrow + 8 * (g + 4));
+
+    f32x4 s[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      const EVT_LDS char* kr = Ks + (kt * 16 + c16) * ROWB;
+      const u32x4 k0 = *(const EVT_LDS u32x4*)(kr + ((g ^ sw) * 16));
+      const u32x4 k1 = *(const EVT_LDS u32x4*)(kr + (((g + 4) ^ sw) * 16));
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, k0),
+                                                    __builtin_bit_cast(bf16x8, qf0), acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, k1),
+                                                    __builtin_bit_cast(bf16x8, qf1), acc, 0, 0, 0);
+      s[kt] = acc;
+    }
+    // s[kt][j] = S^T[key = kt*16 + 4g + j][query = qt*16 + c16]
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = kt * 16 + 4 * g + j;
+        if (key >= p.N) s[kt][j] = -INFINITY;
+        mx = fmaxf(mx, s[kt][j]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float moff = mx * p.scale_log2;
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float e = __builtin_amdgcn_exp2f(s[kt][j] * p.scale_log2 - moff);
+        s[kt][j] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // transposed-read addressing: lane 16g + 4q + pp reads row 4g+q, cols dt*16 + 4pp .. +3
+    const int tq = (lane >> 2) & 3, tp = lane & 3;
+#pragma unroll
+    for (int ks = 0; ks < NKT / 2; ++ks) {
+      bf16x8 pf;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pf[j] = (bf16)s[2 * ks][j];
+        pf[4 + j] = (bf16)s[2 * ks + 1][j];
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep each step's tr-reads next to their MFMAs
+      const int key0 = ks * 32 + 4 * g + tq;  // key0 & 7 == key1 & 7
+      const int ksw = key0 & 7;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int chunk = 2 * dt + (tp >> 1);
+        const int off = ((chunk ^ ksw) * 16) + (tp & 1) * 8;
+        const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (EVT_LDS i16x4*)(Vs + key0 * ROWB + off));
+        const i16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (EVT_LDS i16x4*)(Vs + (key0 + 16) * ROWB + off));
+        const i16x8 vv = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[dt],
+                                                        0, 0, 0);
+      }
+    }
+    // o[dt][j] = O^T[d = dt*16 + 4g + j][query]
+    const int q = qt * 16 + c16;
+    if (q < p.N) {
+      const float inv = 1.0f / sum;
+      bf16* op = (bf16*)p.out + ((int64_t)b * p.N + q) * p.ldo + h * 64 + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) store4(op + dt * 16, o[dt] * inv);
+    }
+  }
+}
+
+template <int NKT>
+__global__ __launch_bounds__(256) void attn_f32_kernel(AttnParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NP = NKT * 16;
+  constexpr int ROWB = 256;  // 64 fp32
+  EVT_LDS char* Ks = (EVT_LDS char*)smem;
+  EVT_LDS char* Vs = Ks + NP * ROWB;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x / p.H, h = blockIdx.x - b * p.H;
+  const float* qkv = (const float*)p.qkv + (int64_t)b * p.N * p.ldq;
+
+  {
+    const int srow = lane >> 4, sslot = lane & 15;  // 4 rows of 256 B per wave-instruction
+    for (int i = wave; i < NP / 4; i += 4) {
+      const int row = i * 4 + srow;
+      const int gr = min(row, p.N - 1);
+      const float* rp = qkv + (int64_t)gr * p.ldq + ((sslot ^ (row & 15)) * 4);
+      glds16(rp + (p.H + h) * 64, Ks + i * 4 * ROWB);
+      glds16(rp + (2 * p.H + h) * 64, Vs + i * 4 * ROWB);
+    }
+    wait_vmcnt0();
+    __syncthreads();
+  }
+
+  const int g = lane >> 4, c16 = lane & 15;
+  const int nqt = (p.N + 15) >> 4;
+  for (int qt = wave; qt < nqt; qt += 4) {
+    const int qi = min(qt * 16 + c16, p.N - 1);
+    const float* qrow = qkv + (int64_t)qi * p.ldq + h * 64;
+    f32x4 qf[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) qf[kk] = *(const f32x4*)(qrow + 4 * (g + 4 * kk));
+
+    f32x4 s[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      const int row = kt * 16 + c16;
+      const EVT_LDS char* kr = Ks + row * ROWB;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const f32x4 kf = *(const EVT_LDS f32x4*)(kr + (((g + 4 * kk) ^ (row & 15)) * 16));
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[e], qf[kk][e], acc, 0, 0, 0);
+      }
+      s[kt] = acc;
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = kt * 16 + 4 * g + j;
+        if (key >= p.N) s[kt][j] = -INFINITY;
+        mx = fmaxf(mx, s[kt][j]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float moff = mx * p.scale_log2;
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float e = exp2f(s[kt][j] * p.scale_log2 - moff);
+        s[kt][j] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        __builtin_amdgcn_sched_barrier(0);
+        const int key = kt * 16 + 4 * g + e;
+        const EVT_LDS char* vr = Vs + key * ROWB;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const int d = dt * 16 + c16;
+          const float v = *(const EVT_LDS float*)(vr + (((d >> 2) ^ (key & 15)) * 16) + (d & 3) * 4);
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, s[kt][e], o[dt], 0, 0, 0);
+        }
+      }
+    const int q = qt * 16 + c16;
+    if (q < p.N) {
+      const float inv = 1.0f / sum;
+      float* op = (float*)p.out + ((int64_t)b * p.N + q) * p.ldo + h * 64 + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) store4(op + dt * 16, o[dt] * inv);
+    }
+  }
+}
+
+template <int NKT>
+hipError_t launch_nkt(int dtype, const AttnParams& p, hipStream_t s) {
+  const int rowb = dtype == DT_BF16 ? 128 : 256;
+  const size_t lds = 2 * (size_t)NKT * 16 * rowb;
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(attn_bf16_kernel<NKT>, dim3(p.B * p.H), dim3(256), lds, s, p);
+  else
+    hipLaunchKernelGGL(attn_f32_kernel<NKT>, dim3(p.B * p.H), dim3(256), lds, s, p);
+  return hipGetLastError();
+}
+
+bool g_attr_set = false;
+
+void set_lds_attrs() {
+  if (g_attr_set) return;
+  g_attr_set = true;
+  hipFuncSetAttribute((const void*)attn_f32_kernel<14>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      2 * 14 * 16 * 256);
+  hipFuncSetAttribute((const void*)attn_f32_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      2 * 16 * 16 * 256);
+}
+
+}  // namespace
+
+hipError_t attention_launch(int dtype, const AttnParams& p, hipStream_t s) {
+  if (p.B <= 0) return hipSuccess;
+  if (p.N <= 0 || p.N > 256 || p.H <= 0) return hipErrorInvalidValue;
+  set_lds_attrs();
+  if (p.N <= 64) return launch_nkt<4>(dtype, p, s);
+  if (p.N <= 128) return launch_nkt<8>(dtype, p, s);
+  if (p.N <= 224) return launch_nkt<14>(dtype, p, s);
+  return launch_nkt<16>(dtype, p, s);
+}
+
+}  // namespace evt

@@ -1,0 +1,161 @@
+// Memory-bound kernels of the ViT forward on gfx950: LayerNorm, patchify (+CLS row), CLS gather.
+//
+// LayerNorm replaces Keras LayerNormalization(epsilon=1e-5) of reference
+// `modeling/layers/norm.py:6,12`: population variance over the last axis, fp32 statistics.
+// One wave64 per token row, 16-B loads, the row held in registers (D <= 1024), two-pass mean /
+// variance with butterfly wave reductions; output written in the activation dtype (bf16 feeds the
+// next MFMA GEMM directly and is also that sublayer's residual, reference `residual.py:9`).
+//
+// patchify replaces the einops Rearrange 'b c (h p1) (w p2) -> b (h w) (p1 p2 c)' of reference
+// `modeling/models/vit.py:31-32,45`: one workgroup per (image, patch-row) stages the
+// [C][ps][W] strip of the NCHW image in LDS with coalesced 16-B loads, then writes the 14 patch
+// vectors of that row coalesced in (p1 p2 c) order. The first strip of each image also writes the
+// CLS token row x[b, 0] = cls + pos[0] (reference vit.py:48-51) into the fp32 token stream.
+#include "common.h"
+#include "evt_internal.h"
+
+namespace evt {
+
+namespace {
+
+template <typename TO, int NV>  // NV = float4 groups per lane (D <= 256*NV)
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int64_t ldx,
+                                                        TO* __restrict__ y, int64_t ldy,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, int rows,
+                                                        int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + (int64_t)row * ldx;
+  f32x4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    v[i] = c < D ? load4(xr + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+  }
+  const float inv_d = 1.0f / (float)D;
+  const float mean = wave_sum(s) * inv_d;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < D) {
+      const f32x4 d = v[i] - mean;
+      q += d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3];
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) * inv_d + eps);
+  TO* yr = y + (int64_t)row * ldy;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < D) store4(yr + c, (v[i] - mean) * rstd * load4(gamma + c) + load4(beta + c));
+  }
+}
+
+// grid (HW/ps, B); block 256. LDS strip [C][ps][HW] fp32.
+template <typename TO>
+__global__ __launch_bounds__(256) void patchify_kernel(const float* __restrict__ img, int C, int HW,
+                                                       int ps, TO* __restrict__ out,
+                                                       float* __restrict__ x,
+                                                       const float* __restrict__ cls,
+                                                       const float* __restrict__ pos, int D) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* strip = (float*)smem;
+  const int hh = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int np = HW / ps;
+  // stage rows hh*ps .. hh*ps+ps-1 of every channel (contiguous ps*HW floats per channel)
+  const int per_c = ps * HW;  // multiple of 4 (HW % 4 == 0 checked on host)
+  for (int c = 0; c < C; ++c) {
+    const float* src = img + (((int64_t)b * C + c) * HW + (int64_t)hh * ps) * HW;
+    for (int i = tid * 4; i < per_c; i += 256 * 4) *(f32x4*)(strip + c * per_c + i) = load4(src + i);
+  }
+  __syncthreads();
+  const int pd = ps * ps * C;  // patch vector length
+  TO* orow = out + ((int64_t)b * np * np + (int64_t)hh * np) * pd;
+  for (int e = tid; e < np * pd; e += 256) {
+    const int ww = e / pd, f = e - ww * pd;
+    const int c = f % C, p12 = f / C, p1 = p12 / ps, p2 = p12 - p1 * ps;
+    orow[(int64_t)ww * pd + f] = from_f32<TO>(strip[c * per_c + p1 * HW + ww * ps + p2]);
+  }
+  if (hh == 0) {
+    float* xr = x + (int64_t)b * (np * np + 1) * D;
+    for (int n = tid; n < D; n += 256) xr[n] = cls[n] + pos[n];
+  }
+}
+
+template <typename TO>
+__global__ void gather_cls_kernel(const float* __restrict__ x, int64_t stride, int B, int D,
+                                  TO* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * D) return;
+  const int b = i / D, n = i - b * D;
+  out[i] = from_f32<TO>(x[(int64_t)b * stride + n]);
+}
+
+template <typename TO, int NV>
+hipError_t ln_nv(const float* x, int64_t ldx, void* y, int64_t ldy, const float* g,
+                 const float* bb, int rows, int D, float eps, hipStream_t s) {
+  hipLaunchKernelGGL((layernorm_kernel<TO, NV>), dim3((rows + 3) / 4), dim3(256), 0, s, x, ldx,
+                     (TO*)y, ldy, g, bb, rows, D, eps);
+  return hipGetLastError();
+}
+
+template <typename TO>
+hipError_t ln_t(const float* x, int64_t ldx, void* y, int64_t ldy, const float* g, const float* bb,
+                int rows, int D, float eps, hipStream_t s) {
+  if (D <= 256) return ln_nv<TO, 1>(x, ldx, y, ldy, g, bb, rows, D, eps, s);
+  if (D <= 512) return ln_nv<TO, 2>(x, ldx, y, ldy, g, bb, rows, D, eps, s);
+  if (D <= 768) return ln_nv<TO, 3>(x, ldx, y, ldy, g, bb, rows, D, eps, s);
+  return ln_nv<TO, 4>(x, ldx, y, ldy, g, bb, rows, D, eps, s);
+}
+
+}  // namespace
+
+hipError_t layernorm_launch(int dtype, const float* x, int64_t ldx, void* y, int64_t ldy,
+                            const float* gamma, const float* beta, int rows, int D, float eps,
+                            hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  if (D <= 0 || D > 1024 || (D & 3) || (ldx & 3) || (ldy & 3)) return hipErrorInvalidValue;
+  return dtype == DT_BF16 ? ln_t<bf16>(x, ldx, y, ldy, gamma, beta, rows, D, eps, s)
+                          : ln_t<float>(x, ldx, y, ldy, gamma, beta, rows, D, eps, s);
+}
+
+hipError_t patchify_launch(int dtype, const float* img, int B, int C, int HW, int ps, void* out,
+                           float* x, const float* cls, const float* pos, int D, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  if (HW % ps || (ps * HW) % 4) return hipErrorInvalidValue;
+  const size_t lds = (size_t)C * ps * HW * sizeof(float);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  dim3 grid(HW / ps, B);
+  if (dtype == DT_BF16) {
+    hipFuncSetAttribute((const void*)patchify_kernel<bf16>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(patchify_kernel<bf16>, grid, dim3(256), lds, s, img, C, HW, ps, (bf16*)out,
+                       x, cls, pos, D);
+  } else {
+    hipFuncSetAttribute((const void*)patchify_kernel<float>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(patchify_kernel<float>, grid, dim3(256), lds, s, img, C, HW, ps,
+                       (float*)out, x, cls, pos, D);
+  }
+  return hipGetLastError();
+}
+
+hipError_t gather_cls_launch(int dtype, const float* x, int64_t row_stride, int B, int D, void* out,
+                             hipStream_t s) {
+  const int n = B * D;
+  if (n <= 0) return hipSuccess;
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(gather_cls_kernel<bf16>, dim3((n + 255) / 256), dim3(256), 0, s, x,
+                       row_stride, B, D, (bf16*)out);
+  else
+    hipLaunchKernelGGL(gather_cls_kernel<float>, dim3((n + 255) / 256), dim3(256), 0, s, x,
+                       row_stride, B, D, (float*)out);
+  return hipGetLastError();
+}
+
+}  // namespace evt

@@ -1,0 +1,154 @@
+"""Deterministic parameter and input generation for the ViT family.
+
+The reference never loads trained weights for its `modeling.models` forward: every
+parameter is random-initialised by Keras (`modeling/models/vit.py:18-29`,
+`modeling/models/t2t_vit.py:116-118` "not needed when only measuring inference latency").
+This module is the MI355X build's equivalent: a seeded, platform-independent generator
+(numpy PCG64) so the GPU box, the oracle and the golden fixtures all see bit-identical
+fp32 parameters without shipping megabytes of weights.
+
+Parameter layout is the Keras one (`Dense.kernel` is ``[in, out]``, ``y = x @ W + b``),
+named after the reference attributes:
+
+==========================  =========================  ==========================================
+name                        shape                      reference
+==========================  =========================  ==========================================
+``patch_w`` / ``patch_b``   ``[p*p*c, D]`` / ``[D]``   ``patch_to_embedding`` vit.py:23
+``cls``                     ``[D]``                    ``cls_token [1,1,D]`` vit.py:24-29
+``pos``                     ``[P+1, D]``               ``pos_embedding`` vit.py:18-22
+``l{i}.ln1_g/ln1_b``        ``[D]``                    attention-side ``LayerNorm`` norm.py:6
+``l{i}.qkv_w``              ``[D, 3*h*hk]``            ``Attention.to_qkv`` (no bias) attention.py:17
+``l{i}.out_w/out_b``        ``[h*hk, D]`` / ``[D]``    ``Attention.to_out`` attention.py:18
+``l{i}.ln2_g/ln2_b``        ``[D]``                    FFN-side ``LayerNorm`` norm.py:6
+``l{i}.fc1_w/fc1_b``        ``[D, F]`` / ``[F]``       ``FeedForward`` Dense 1 ffn.py:8
+``l{i}.fc2_w/fc2_b``        ``[F, D]`` / ``[D]``       ``FeedForward`` Dense 2 ffn.py:9
+``head1_w/head1_b``         ``[D, M]`` / ``[M]``       ``mlp_head[0]`` vit.py:38
+``head2_w/head2_b``         ``[M, C]`` / ``[C]``       ``mlp_head[1]`` vit.py:39
+==========================  =========================  ==========================================
+
+Initialisers (Keras-like, with non-zero biases on purpose so every bias path is exercised):
+glorot-uniform kernels, biases ~ N(0, 0.02), gamma = 1 + N(0, 0.02), beta ~ N(0, 0.02),
+cls / pos ~ N(0, 0.05) (the Keras ``RandomNormal`` default, vit.py:21,28).
+"""
+from __future__ import annotations
+
+import hashlib
+from dataclasses import dataclass, field
+from typing import Dict, List, Sequence
+
+import numpy as np
+
+
+@dataclass(frozen=True)
+class ViTConfig:
+    """Static shape of a `ViT` / `ViT_Pruned` (reference `modeling/models/vit.py:11-75`)."""
+
+    image_size: int = 224
+    patch_size: int = 16
+    in_chans: int = 3
+    num_classes: int = 1000
+    dim: int = 768
+    depth: int = 12
+    mlp_dim: int = 3072           # head MLP width; also the unpruned FFN width
+    heads: Sequence[int] = field(default_factory=lambda: (12,) * 12)   # per layer
+    head_dim: Sequence[int] = field(default_factory=lambda: (64,) * 12)  # per layer h_k
+    ffn: Sequence[int] = field(default_factory=lambda: (3072,) * 12)    # per layer width
+
+    @property
+    def num_patches(self) -> int:
+        return (self.image_size // self.patch_size) ** 2
+
+    @property
+    def tokens(self) -> int:
+        return self.num_patches + 1
+
+    @property
+    def patch_dim(self) -> int:
+        return self.patch_size * self.patch_size * self.in_chans
+
+    def gflop_per_image(self) -> float:
+        """Matmul FLOPs (2*MAC) of one image's forward; the roofline's algorithmic work."""
+        n, p, d = self.tokens, self.num_patches, self.dim
+        f = 2.0 * p * self.patch_dim * d
+        for i in range(self.depth):
+            inner = self.heads[i] * self.head_dim[i]
+            f += 2.0 * n * d * 3 * inner              # QKV
+            f += 2.0 * 2 * n * n * inner              # QK^T and P.V
+            f += 2.0 * n * inner * d                  # out-proj
+            f += 2.0 * 2 * n * d * self.ffn[i]        # FC1 + FC2
+        f += 2.0 * d * self.mlp_dim + 2.0 * self.mlp_dim * self.num_classes
+        return f / 1e9
+
+
+def vit_config(dim: int, depth: int, heads: int, mlp_dim: int, *, image_size=224, patch_size=16,
+               num_classes=1000, head_size: int | None = None,
+               heads_list: Sequence[int] | None = None,
+               ffn_list: Sequence[int] | None = None) -> ViTConfig:
+    hk = head_size if head_size is not None else dim // heads
+    hl = tuple(heads_list) if heads_list is not None else (heads,) * depth
+    fl = tuple(ffn_list) if ffn_list is not None else (mlp_dim,) * depth
+    return ViTConfig(image_size=image_size, patch_size=patch_size, num_classes=num_classes,
+                     dim=dim, depth=depth, mlp_dim=mlp_dim, heads=hl,
+                     head_dim=(hk,) * depth, ffn=fl)
+
+
+def _glorot(rng: np.random.Generator, fan_in: int, fan_out: int) -> np.ndarray:
+    lim = np.sqrt(6.0 / (fan_in + fan_out))
+    return rng.uniform(-lim, lim, size=(fan_in, fan_out))
+
+
+def vit_param_shapes(cfg: ViTConfig) -> List[tuple]:
+    """Ordered (name, shape) list; this order is also the C-ABI weight-pointer order."""
+    d = cfg.dim
+    out = [("patch_w", (cfg.patch_dim, d)), ("patch_b", (d,)), ("cls", (d,)),
+           ("pos", (cfg.tokens, d))]
+    for i in range(cfg.depth):
+        inner = cfg.heads[i] * cfg.head_dim[i]
+        f = cfg.ffn[i]
+        out += [(f"l{i}.ln1_g", (d,)), (f"l{i}.ln1_b", (d,)),
+                (f"l{i}.qkv_w", (d, 3 * inner)),
+                (f"l{i}.out_w", (inner, d)), (f"l{i}.out_b", (d,)),
+                (f"l{i}.ln2_g", (d,)), (f"l{i}.ln2_b", (d,)),
+                (f"l{i}.fc1_w", (d, f)), (f"l{i}.fc1_b", (f,)),
+                (f"l{i}.fc2_w", (f, d)), (f"l{i}.fc2_b", (d,))]
+    out += [("head1_w", (d, cfg.mlp_dim)), ("head1_b", (cfg.mlp_dim,)),
+            ("head2_w", (cfg.mlp_dim, cfg.num_classes)), ("head2_b", (cfg.num_classes,))]
+    return out
+
+
+def make_vit_params(cfg: ViTConfig, seed: int = 0) -> Dict[str, np.ndarray]:
+    """Seeded fp32 parameters for `cfg` (same values on every platform)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    params: Dict[str, np.ndarray] = {}
+    for name, shape in vit_param_shapes(cfg):
+        leaf = name.split(".")[-1]
+        if leaf.endswith("_w"):
+            v = _glorot(rng, shape[0], shape[1])
+        elif leaf.endswith("_g"):
+            v = 1.0 + rng.normal(0.0, 0.02, size=shape)
+        elif leaf in ("cls", "pos"):
+            v = rng.normal(0.0, 0.05, size=shape)
+        else:  # biases, LN beta
+            v = rng.normal(0.0, 0.02, size=shape)
+        params[name] = np.ascontiguousarray(v, dtype=np.float32)
+    return params
+
+
+def make_images(batch: int, seed: int = 1, image_size: int = 224, chans: int = 3,
+                layout: str = "NCHW") -> np.ndarray:
+    """Seeded N(0,1) fp32 images, the distribution of `tools.py:204` / `utils.py:482`."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    x = rng.standard_normal((batch, chans, image_size, image_size), dtype=np.float32)
+    if layout == "NHWC":
+        x = np.ascontiguousarray(x.transpose(0, 2, 3, 1))
+    return x
+
+
+def digest(arrays: Dict[str, np.ndarray] | Sequence[np.ndarray]) -> str:
+    """SHA-256 over the raw bytes (in order) - pins generator output in fixtures."""
+    h = hashlib.sha256()
+    items = arrays.items() if isinstance(arrays, dict) else enumerate(arrays)
+    for k, v in items:
+        h.update(str(k).encode())
+        h.update(np.ascontiguousarray(v).tobytes())
+    return h.hexdigest()

@@ -1,0 +1,73 @@
+"""Thin test helpers that call the op-level C ABI (include/evt.h) on torch device tensors."""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from edgevisiontransformer_amd import _lib
+
+TDT = {"f32": torch.float32, "bf16": torch.bfloat16}
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr() if t is not None else 0)
+
+
+def _s():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def round_up(x, m):
+    return (x + m - 1) // m * m
+
+
+def pack(W: torch.Tensor, dtype: str) -> tuple:
+    """Keras [K, N] fp32 (device) -> packed [Npad][Kpad]."""
+    K, N = W.shape
+    kpad, npad = round_up(K, 64), round_up(N, 128)
+    wp = torch.empty((npad, kpad), dtype=TDT[dtype], device=W.device)
+    _lib.check(_lib.load_library().evt_pack_weight(_lib.DTYPE[dtype], _p(W.contiguous()), K, N,
+                                                    _p(wp), kpad, npad, _s()))
+    return wp, kpad, npad
+
+
+def dense(dtype, flags, A, wp, kpad, npad, M, N, ldc=None, bias=None, resid=None, pos=None, P=0,
+          C=None):
+    out_f32 = bool(flags & _lib.EPI_OUT_F32)
+    ldc = ldc or N
+    if C is None:
+        rows = M if not (flags & _lib.EPI_POS) else (M // P) * (P + 1)
+        C = torch.zeros((rows, ldc), dtype=torch.float32 if out_f32 else TDT[dtype], device=A.device)
+    _lib.check(_lib.load_library().evt_dense(
+        _lib.DTYPE[dtype], flags, _p(A), A.stride(0), _p(wp), kpad, npad, _p(C), ldc, M, N,
+        _p(bias), _p(resid), resid.stride(0) if resid is not None else 0, _p(pos),
+        pos.stride(0) if pos is not None else 0, P, _s()))
+    return C
+
+
+def attention(dtype, qkv, B, N, H, scale=0.125, out=None):
+    if out is None:
+        out = torch.zeros((B * N, H * 64), dtype=TDT[dtype], device=qkv.device)
+    _lib.check(_lib.load_library().evt_attention(_lib.DTYPE[dtype], _p(qkv), qkv.stride(0), _p(out),
+                                                 out.stride(0), B, N, H, scale, _s()))
+    return out
+
+
+def layernorm(dtype, x, gamma, beta, eps=1e-5):
+    rows, D = x.shape
+    y = torch.empty((rows, D), dtype=TDT[dtype], device=x.device)
+    _lib.check(_lib.load_library().evt_layernorm(_lib.DTYPE[dtype], _p(x), x.stride(0), _p(y),
+                                                 y.stride(0), _p(gamma), _p(beta), rows, D, eps,
+                                                 _s()))
+    return y
+
+
+def patchify(dtype, img, ps, cls, pos, D):
+    B, C, HW, _ = img.shape
+    P = (HW // ps) ** 2
+    out = torch.empty((B * P, ps * ps * C), dtype=TDT[dtype], device=img.device)
+    x = torch.zeros((B * (P + 1), D), dtype=torch.float32, device=img.device)
+    _lib.check(_lib.load_library().evt_patchify(_lib.DTYPE[dtype], _p(img), B, C, HW, ps, _p(out),
+                                                _p(x), _p(cls), _p(pos), D, _s()))
+    return out, x

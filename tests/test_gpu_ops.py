@@ -1,0 +1,151 @@
+"""Kernel-level parity on the GPU: each HIP kernel vs an fp64 CPU restatement of the same op on
+the same (dtype-rounded) inputs. Tolerances are stated per dtype in each test."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from edgevisiontransformer_amd import _lib
+from oracle import vit_ref
+from tests import _ops
+
+pytestmark = pytest.mark.gpu
+
+# bf16 output rounding is 2^-9 relative; fp32 MFMA is an exact f32 fmaf chain.
+TOL = {"bf16": dict(rtol=1.6e-2, atol=1.6e-2), "f32": dict(rtol=5e-5, atol=5e-5)}
+
+
+def _rand(shape, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(shape, generator=g, dtype=torch.float64) * scale
+
+
+def _q(t64, dtype):
+    """Round an fp64 CPU tensor to the kernel dtype and back (what the kernel actually sees)."""
+    return t64.to(_ops.TDT[dtype]).to(torch.float64)
+
+
+def _gelu(x):
+    return x * 0.5 * (1.0 + torch.tanh(math.sqrt(2 / math.pi) * (x + 0.044715 * x ** 3)))
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("M,K,N", [(197, 192, 576), (394, 768, 2304), (131, 320, 37 * 4),
+                                   (1000, 576, 192), (64, 64, 1000), (257, 3072, 768)])
+@pytest.mark.parametrize("flags", [0, 3, 21, 17])
+def test_dense(gpu, dtype, M, K, N, flags):
+    A64 = _rand((M, K), 1)
+    W64 = _rand((K, N), 2, scale=1.0 / math.sqrt(K))
+    b64 = _rand((N,), 3, scale=0.1)
+    R64 = _rand((M, N), 4)
+    A = A64.to(_ops.TDT[dtype]).to(gpu)
+    W = W64.float().to(gpu)
+    wp, kpad, npad = _ops.pack(W, dtype)
+    kw = {}
+    if flags & _lib.EPI_BIAS:
+        bias = torch.zeros(npad, dtype=torch.float32, device=gpu)
+        bias[:N] = b64.float().to(gpu)
+        kw["bias"] = bias
+    if flags & _lib.EPI_RESID:
+        kw["resid"] = R64.to(_ops.TDT[dtype]).to(gpu)
+    if kpad != K:
+        Ap = torch.zeros((M, kpad), dtype=A.dtype, device=gpu)
+        Ap[:, :K] = A
+        A = Ap
+    C = _ops.dense(dtype, flags, A, wp, kpad, npad, M, N, **kw)
+    torch.cuda.synchronize()
+    ref = _q(A64, dtype) @ _q(W64.float().double(), dtype)
+    if flags & _lib.EPI_BIAS:
+        ref = ref + b64.float().double()
+    if flags & _lib.EPI_GELU:
+        ref = _gelu(ref)
+    if flags & _lib.EPI_RESID:
+        ref = ref + _q(R64, dtype)
+    got = C.double().cpu()
+    tol = TOL["f32"] if (dtype == "f32") else (TOL["bf16"] if not (flags & _lib.EPI_OUT_F32)
+                                                else dict(rtol=1e-3, atol=1e-3))
+    torch.testing.assert_close(got, ref, **tol)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+def test_dense_patch_embed_remap(gpu, dtype):
+    B, P, K, N = 3, 196, 768, 192
+    A64, W64, b64 = _rand((B * P, K), 5), _rand((K, N), 6, 1 / 28.0), _rand((N,), 7, 0.1)
+    pos64 = _rand((P + 1, N), 8, 0.05)
+    A = A64.to(_ops.TDT[dtype]).to(gpu)
+    wp, kpad, npad = _ops.pack(W64.float().to(gpu), dtype)
+    bias = torch.zeros(npad, device=gpu)
+    bias[:N] = b64.float().to(gpu)
+    pos = pos64.float().to(gpu)
+    C = torch.full((B * (P + 1), N), 7.0, device=gpu)
+    _ops.dense(dtype, _lib.EPI_BIAS | _lib.EPI_POS | _lib.EPI_OUT_F32, A, wp, kpad, npad, B * P, N,
+               bias=bias, pos=pos, P=P, C=C)
+    torch.cuda.synchronize()
+    ref = (_q(A64, dtype) @ _q(W64.float().double(), dtype) + b64.float().double()).reshape(B, P, N)
+    ref = ref + pos64.float().double()[1:]
+    got = C.double().cpu().reshape(B, P + 1, N)
+    assert torch.all(got[:, 0] == 7.0), "CLS rows must be left untouched by the patch GEMM"
+    torch.testing.assert_close(got[:, 1:], ref, rtol=1e-3, atol=1e-3)
+
+
+def _attn_ref(qkv64, B, N, H):
+    q, k, v = qkv64.reshape(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = torch.einsum("bhid,bhjd->bhij", q, k) * 0.125
+    p = torch.softmax(s, dim=-1)
+    return torch.einsum("bhij,bhjd->bhid", p, v).permute(0, 2, 1, 3).reshape(B * N, H * 64)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("B,N,H", [(2, 197, 3), (1, 197, 12), (3, 50, 2), (2, 256, 1),
+                                   (1, 1, 2), (2, 129, 4), (1, 224, 6)])
+def test_attention(gpu, dtype, B, N, H):
+    qkv64 = _rand((B * N, 3 * H * 64), 11, scale=1.5)
+    qkv = qkv64.to(_ops.TDT[dtype]).to(gpu)
+    out = _ops.attention(dtype, qkv, B, N, H)
+    torch.cuda.synchronize()
+    ref = _attn_ref(_q(qkv64, dtype), B, N, H)
+    tol = dict(rtol=2e-2, atol=2e-2) if dtype == "bf16" else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(out.double().cpu(), ref, **tol)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+def test_attention_peaked_softmax(gpu, dtype):
+    """One key dominates every query (scores ~ +40): exercises the max-subtraction path."""
+    B, N, H = 1, 197, 2
+    qkv64 = _rand((B * N, 3 * H * 64), 12, scale=0.2)
+    qkv64[:, : H * 64] += 1.0   # q
+    qkv64[5, H * 64: 2 * H * 64] += 5.0  # key 5 spikes
+    qkv = qkv64.to(_ops.TDT[dtype]).to(gpu)
+    out = _ops.attention(dtype, qkv, B, N, H)
+    torch.cuda.synchronize()
+    ref = _attn_ref(_q(qkv64, dtype), B, N, H)
+    tol = dict(rtol=2e-2, atol=2e-2) if dtype == "bf16" else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(out.double().cpu(), ref, **tol)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("rows,D", [(197, 192), (394, 384), (1000, 768), (3, 64), (5, 1024)])
+def test_layernorm(gpu, dtype, rows, D):
+    x64 = _rand((rows, D), 21, 3.0) + 0.5
+    g64, b64 = 1.0 + _rand((D,), 22, 0.1), _rand((D,), 23, 0.1)
+    y = _ops.layernorm(dtype, x64.float().to(gpu), g64.float().to(gpu), b64.float().to(gpu))
+    torch.cuda.synchronize()
+    ref = torch.from_numpy(vit_ref.layer_norm(x64.float().double().numpy(), g64.float().double().numpy(),
+                                              b64.float().double().numpy()))
+    tol = TOL["bf16"] if dtype == "bf16" else dict(rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(y.double().cpu(), ref, **tol)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+def test_patchify(gpu, dtype):
+    B, C, HW, ps, D = 2, 3, 224, 16, 192
+    img = _rand((B, C, HW, HW), 31).float()
+    cls, pos = _rand((D,), 32).float(), _rand((197, D), 33).float()
+    out, x = _ops.patchify(dtype, img.to(gpu), ps, cls.to(gpu), pos.to(gpu), D)
+    torch.cuda.synchronize()
+    ref = vit_ref.patchify_nchw(img.numpy(), ps).reshape(B * 196, -1)
+    exp = torch.from_numpy(ref).to(_ops.TDT[dtype])
+    assert torch.equal(out.cpu(), exp), "patchify is a pure permutation: must be bit-exact"
+    xr = x.cpu().reshape(B, 197, D)
+    assert torch.equal(xr[:, 0], (cls + pos[0]).expand(B, D))
