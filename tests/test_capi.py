@@ -1,0 +1,63 @@
+"""CPU: libevt_hip.so loads and exports every entry point include/evt.h declares; host-only
+validation paths return the documented error codes without touching a GPU."""
+import ctypes
+import os
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "evt.h")
+
+
+def _declared():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(evt_\w+)\(", txt, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from edgevisiontransformer_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        from edgevisiontransformer_amd.build import build
+        build()
+    return _lib.load_library()
+
+
+def test_header_and_binding_agree():
+    from edgevisiontransformer_amd import _lib
+    assert _declared() == sorted(_lib.SIGNATURES)
+    assert len(_declared()) == 12
+
+
+def test_every_declared_symbol_is_exported(lib):
+    for name in _declared():
+        assert hasattr(lib, name), name
+
+
+def test_host_validation_codes(lib):
+    from edgevisiontransformer_amd import _lib
+    arr = (ctypes.c_int32 * 12)(*([12] * 12))
+    hd = (ctypes.c_int32 * 12)(*([64] * 12))
+    ffn = (ctypes.c_int32 * 12)(*([3072] * 12))
+    d = _lib.evt_vit_desc(224, 16, 3, 1000, 768, 12, 3072, arr, hd, ffn, 1, 512)
+    assert lib.evt_vit_num_weights(ctypes.byref(d)) == 4 + 11 * 12 + 4
+    out = ctypes.c_size_t()
+    assert lib.evt_query_workspace(ctypes.byref(d), 512, ctypes.byref(out)) == 0
+    assert 1.5e9 < out.value < 3e9  # ~1.9 GB of activations for DeiT-base bs512 bf16
+    bad = _lib.evt_vit_desc(225, 16, 3, 1000, 768, 12, 3072, arr, hd, ffn, 1, 512)
+    assert lib.evt_query_workspace(ctypes.byref(bad), 512, ctypes.byref(out)) == _lib.EVT_EINVAL
+    assert b"divisible by the patch size" in lib.evt_last_error()
+    hd2 = (ctypes.c_int32 * 12)(*([32] * 12))
+    bad2 = _lib.evt_vit_desc(224, 16, 3, 1000, 768, 12, 3072, arr, hd2, ffn, 1, 512)
+    assert lib.evt_query_workspace(ctypes.byref(bad2), 1, ctypes.byref(out)) == _lib.EVT_EINVAL
+    out_h = ctypes.c_void_p()
+    assert lib.evt_vit_create(ctypes.byref(d), None, 0, None, ctypes.byref(out_h)) == _lib.EVT_EINVAL
+    assert lib.evt_model_destroy(None) == 0
+
+
+def test_op_entry_points_validate_before_launch(lib):
+    from edgevisiontransformer_amd import _lib
+    assert lib.evt_attention(1, None, 0, None, 0, 1, 197, 3, 0.125, None) == _lib.EVT_EINVAL
+    assert lib.evt_layernorm(1, None, 0, None, 0, None, None, 1, 7, 1e-5, None) == _lib.EVT_EINVAL
+    assert lib.evt_pack_weight(1, None, 1, 1, None, 64, 128, None) == _lib.EVT_EINVAL
