@@ -60,7 +60,7 @@ def kernel_probe(dtype: str, M: int, K: int, N: int, iters: int = 20) -> float:
     g = torch.Generator(device=dev).manual_seed(123)
     A = torch.randn((M, K), generator=g, device=dev).to(tdt)
     W = torch.randn((K, N), generator=g, device=dev) / K ** 0.5
-    kpad, npad = (K + 63) // 64 * 64, (N + 127) // 128 * 128
+    kpad, npad = (K + 63) // 64 * 64, (N + 255) // 256 * 256
     wp = torch.empty((npad, kpad), dtype=tdt, device=dev)
     bias = torch.zeros(npad, device=dev)
     C = torch.empty((M, N), dtype=tdt, device=dev)

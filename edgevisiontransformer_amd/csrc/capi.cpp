@@ -129,7 +129,7 @@ int make_dense(evt_model* m, DenseW* dw, const float* W, const float* b, int K, 
   dw->K = K;
   dw->N = N;
   dw->kpad = (int)round_up(K, PAD_K);
-  dw->npad = (int)round_up(N, GEMM_BN);
+  dw->npad = (int)round_up(N, PACK_N);
   int rc = dev_alloc(m, &dw->w, (size_t)dw->kpad * dw->npad * elem_size(dt));
   if (rc) return rc;
   EVT_HIP(pack_weight(dt, W, K, N, dw->w, dw->kpad, dw->npad, s), "pack_weight");
@@ -343,6 +343,12 @@ int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* 
 }
 
 // ---- op-level entry points --------------------------------------------------------------
+
+int evt_set_gemm_variant(int variant) {
+  if (variant < 0 || variant > 31) return fail(EVT_EINVAL, "variant must be 0..31");
+  gemm_set_variant(variant);
+  return EVT_OK;
+}
 
 int evt_pack_weight(int dtype, const float* W, int K, int N, void* Wp, int Kpad, int Npad,
                     void* stream) {

@@ -35,13 +35,14 @@ __device__ __forceinline__ void store4(bf16* p, f32x4 v) {
   *(bf16x4*)p = o;
 }
 
-// tanh-approximate GELU in fp32 (reference modeling/layers/activation.py:13-15).
+// tanh-approximate GELU in fp32 (reference modeling/layers/activation.py:13-15), evaluated as
+// x * 0.5 * (1 + tanh(u)) == x * sigmoid(2u) = x / (1 + 2^(-2u*log2 e)): one v_exp_f32 and one
+// v_rcp_f32. Tails saturate cleanly (2^+inf -> inf -> x * 0; 2^-inf -> 0 -> x).
 __device__ __forceinline__ float gelu_tanh(float x) {
-  const float k0 = 0.7978845608028654f;  // sqrt(2/pi)
-  float u = k0 * (x + 0.044715f * x * x * x);
-  // tanh(u) = 1 - 2 / (exp(2u) + 1); exp saturates cleanly to 0 / inf at the tails
-  float t = 1.0f - 2.0f / (__expf(2.0f * u) + 1.0f);
-  return 0.5f * x * (1.0f + t);
+  const float c1 = -2.0f * 0.7978845608028654f * 1.4426950408889634f;  // -2*sqrt(2/pi)*log2(e)
+  const float c3 = c1 * 0.044715f;
+  const float e = __builtin_amdgcn_exp2f(x * (c1 + c3 * x * x));
+  return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
 // Wave64 reductions (butterfly over all 64 lanes).

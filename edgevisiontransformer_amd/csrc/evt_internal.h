@@ -27,10 +27,12 @@ struct GemmParams {
 };
 constexpr int GEMM_BM = 128;
 constexpr int GEMM_BN = 128;
+constexpr int PACK_N = 256;  // packed weight rows are padded to this (both tile shapes divide it)
 constexpr int PAD_K = 64;   // K granularity (elements) of every packed operand
 constexpr int PAD_N = 64;   // column granularity of activation buffers
 
 hipError_t gemm_launch(int dtype, int flags, const GemmParams& p, hipStream_t s);
+void gemm_set_variant(int v);  // 0 auto, 1 force 128x128 tiles, 2 force 256x256 (bf16)
 hipError_t pack_weight(int dtype, const float* W, int K, int N, void* Wp, int Kpad, int Npad,
                        hipStream_t s);
 

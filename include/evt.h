@@ -93,6 +93,10 @@ int evt_model_destroy(evt_model* model);
 
 /* ---- op-level entry points (one per hot-path kernel; used by the parity tests) ---------- */
 
+/* GEMM tile-shape policy for bf16 (process-wide tuning knob): 0 = automatic (256x256 tiles when
+ * the problem fills the chip, else 128x128), 1 = always 128x128, 2 = 256x256 whenever packable. */
+int evt_set_gemm_variant(int variant);
+
 /* Pack a Keras [K, N] fp32 kernel into the GEMM operand layout Wp[Npad][Kpad] (dtype),
  * zero padded. Npad % 128 == 0, Kpad % 64 == 0. */
 int evt_pack_weight(int dtype, const float* W, int K, int N, void* Wp, int Kpad, int Npad,

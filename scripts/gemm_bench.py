@@ -1,0 +1,59 @@
+"""GEMM microbenchmark on the GPU: model-shaped bf16 GEMMs, 128x128 vs 256x256 tile kernels,
+interleaved rounds in one process (HIP events), plus a cross-check of the two variants."""
+import ctypes
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from edgevisiontransformer_amd import _lib  # noqa: E402
+
+lib = _lib.load_library()
+_lib.ensure_device(0)
+S = lambda: ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)  # noqa: E731
+P = lambda t: ctypes.c_void_p(t.data_ptr() if t is not None else 0)  # noqa: E731
+M = int(sys.argv[1]) if len(sys.argv) > 1 else 512 * 197
+VARS = [int(v) for v in sys.argv[2].split(',')] if len(sys.argv) > 2 else [1, 2, 3]
+shapes = {"qkv": (768, 2304, 0), "out": (768, 768, 21), "fc1": (768, 3072, 3), "fc2": (3072, 768, 21),
+          "nt3072": (3072, 768, 0), "nt768x3072": (768, 3072, 0)}
+import os
+shapes = {k: v for k, v in shapes.items() if k in os.environ.get("GS", "qkv,out,fc1,fc2").split(",")}
+res = {}
+g = torch.Generator(device="cuda").manual_seed(0)
+for name, (K, N, fl) in shapes.items():
+    A = torch.randn((M, K), generator=g, device="cuda").bfloat16()
+    W = torch.randn((K, N), generator=g, device="cuda") / K ** 0.5
+    npad = (N + 255) // 256 * 256
+    wp = torch.empty((npad, K), dtype=torch.bfloat16, device="cuda")
+    _lib.check(lib.evt_pack_weight(1, P(W), K, N, P(wp), K, npad, S()))
+    bias = torch.randn(npad, generator=g, device="cuda") * 0.1
+    R = torch.randn((M, N), generator=g, device="cuda").bfloat16()
+    outs = {}
+    for v in VARS:
+        outs[v] = torch.empty((M, N), dtype=torch.float32 if fl & 16 else torch.bfloat16, device="cuda")
+    def run(v):
+        lib.evt_set_gemm_variant(v)
+        _lib.check(lib.evt_dense(1, fl, P(A), K, P(wp), K, npad, P(outs[v]), N, M, N, P(bias),
+                                 P(R) if fl & 4 else ctypes.c_void_p(0), N if fl & 4 else 0,
+                                 ctypes.c_void_p(0), 0, 0, S()))
+    times = {v: [] for v in VARS}
+    for v in VARS:
+        run(v)
+    torch.cuda.synchronize()
+    diff = max((outs[VARS[0]].float() - outs[v].float()).abs().max().item() for v in VARS)
+    for rnd in range(5):
+        for v in VARS:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                run(v)
+            e1.record()
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1) / 10)
+    fl_ = 2.0 * M * N * K
+    res[name] = {f"v{v}": {"ms": round(sorted(t)[2], 4), "tflops": round(fl_ / (sorted(t)[2] / 1e3) / 1e12, 1)}
+                 for v, t in times.items()}
+    res[name]["maxdiff_vs_v1"] = diff
+    print(name, json.dumps(res[name]), flush=True)
+lib.evt_set_gemm_variant(0)

@@ -25,7 +25,7 @@ def round_up(x, m):
 def pack(W: torch.Tensor, dtype: str) -> tuple:
     """Keras [K, N] fp32 (device) -> packed [Npad][Kpad]."""
     K, N = W.shape
-    kpad, npad = round_up(K, 64), round_up(N, 128)
+    kpad, npad = round_up(K, 64), round_up(N, 256)
     wp = torch.empty((npad, kpad), dtype=TDT[dtype], device=W.device)
     _lib.check(_lib.load_library().evt_pack_weight(_lib.DTYPE[dtype], _p(W.contiguous()), K, N,
                                                     _p(wp), kpad, npad, _s()))

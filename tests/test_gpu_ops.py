@@ -34,7 +34,17 @@ def _gelu(x):
 @pytest.mark.parametrize("M,K,N", [(197, 192, 576), (394, 768, 2304), (131, 320, 37 * 4),
                                    (1000, 576, 192), (64, 64, 1000), (257, 3072, 768)])
 @pytest.mark.parametrize("flags", [0, 3, 21, 17])
-def test_dense(gpu, dtype, M, K, N, flags):
+@pytest.mark.parametrize("variant", [1, 2, 0])
+def test_dense(gpu, dtype, M, K, N, flags, variant):
+    """variant 1: 128x128-tile kernel; 2: 256x256-tile kernel (bf16 only; f32 ignores it)."""
+    _lib.load_library().evt_set_gemm_variant(variant)
+    try:
+        _dense_case(gpu, dtype, M, K, N, flags)
+    finally:
+        _lib.load_library().evt_set_gemm_variant(0)
+
+
+def _dense_case(gpu, dtype, M, K, N, flags):
     A64 = _rand((M, K), 1)
     W64 = _rand((K, N), 2, scale=1.0 / math.sqrt(K))
     b64 = _rand((N,), 3, scale=0.1)
