@@ -52,26 +52,38 @@ def parse():
 
 
 def kernel_probe(dtype: str, M: int, K: int, N: int, iters: int = 20) -> float:
-    """Average duration (s) of one FC1-shaped GEMM launch (bias + GELU epilogue), HIP events."""
+    """Average duration (s) of one FC1 GEMM launch exactly as the forward runs it (LayerNorm-
+    folded input, bias, GELU epilogue: flags EPI_LNIN|EPI_BIAS|EPI_GELU), timed with HIP events
+    on the stream the kernel is launched on."""
     from edgevisiontransformer_amd import _lib
     lib = _lib.load_library()
     tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
     dev = torch.device("cuda", torch.cuda.current_device())
     g = torch.Generator(device=dev).manual_seed(123)
-    A = torch.randn((M, K), generator=g, device=dev).to(tdt)
+    x = torch.randn((M, K), generator=g, device=dev)
+    A = x.to(tdt)
+    stats = torch.zeros((M, 2 * ((K + 255) // 256), 2), device=dev)  # include/evt.h slot layout
+    stats[:, 0, 0], stats[:, 0, 1] = x.sum(1), (x * x).sum(1)
     W = torch.randn((K, N), generator=g, device=dev) / K ** 0.5
+    gam, bet = torch.ones(K, device=dev), torch.zeros(K, device=dev)
     kpad, npad = (K + 63) // 64 * 64, (N + 255) // 256 * 256
     wp = torch.empty((npad, kpad), dtype=tdt, device=dev)
-    bias = torch.zeros(npad, device=dev)
+    colsum, cvec = torch.empty(npad, device=dev), torch.empty(npad, device=dev)
     C = torch.empty((M, N), dtype=tdt, device=dev)
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    _lib.check(lib.evt_pack_weight(_lib.DTYPE[dtype], P(W), K, N, P(wp), kpad, npad, s))
+    _lib.check(lib.evt_pack_weight(_lib.DTYPE[dtype], P(W), P(gam), K, N, P(wp), kpad, npad, s))
+    _lib.check(lib.evt_ln_fold(_lib.DTYPE[dtype], P(wp), kpad, npad, P(W), P(bet), None, K, N,
+                               P(colsum), P(cvec), s))
+    a = _lib.evt_dense_args()
+    a.flags = _lib.EPI_LNIN | _lib.EPI_BIAS | _lib.EPI_GELU
+    a.A, a.lda, a.Wp, a.Kpad, a.Npad = A.data_ptr(), K, wp.data_ptr(), kpad, npad
+    a.C, a.ldc, a.M, a.N = C.data_ptr(), N, M, N
+    a.bias, a.colsum, a.stats_in = cvec.data_ptr(), colsum.data_ptr(), stats.data_ptr()
+    a.ln_width, a.ln_eps = K, 1e-5
 
     def launch():
-        _lib.check(lib.evt_dense(_lib.DTYPE[dtype], _lib.EPI_BIAS | _lib.EPI_GELU, P(A), K, P(wp),
-                                 kpad, npad, P(C), N, M, N, P(bias), ctypes.c_void_p(0), 0,
-                                 ctypes.c_void_p(0), 0, 0, s))
+        _lib.check(lib.evt_dense(_lib.DTYPE[dtype], ctypes.byref(a), s))
     for _ in range(3):
         launch()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -163,7 +175,7 @@ def main():
         ach = 2.0 * M * N * K / t_k / 1e12
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(ach / peak, 4), "traffic": None,
-                "kernel": f"gemm_nt_kernel<{args.dtype}, bias+gelu> FC1 M={M} K={K} N={N}",
+                "kernel": f"gemm_big_kernel<LNIN|BIAS|GELU> (FC1, {args.dtype}) M={M} K={K} N={N}",
                 "avg_launch_us": round(t_k * 1e6, 1)}
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

@@ -23,8 +23,9 @@ EVT_EHIP = -5
 EVT_ENODEV = -19
 DTYPE = {"f32": 0, "fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1}
 
-# GEMM epilogue flags (csrc/evt_internal.h)
+# GEMM epilogue flags (include/evt.h EVT_EPI_*)
 EPI_BIAS, EPI_GELU, EPI_RESID, EPI_POS, EPI_OUT_F32 = 1, 2, 4, 8, 16
+EPI_LNIN, EPI_RESLN, EPI_STATS = 32, 64, 128
 
 
 class EvtError(RuntimeError):
@@ -43,6 +44,18 @@ class evt_vit_desc(ctypes.Structure):
                 ("dtype", ctypes.c_int32), ("max_batch", ctypes.c_int32)]
 
 
+class evt_dense_args(ctypes.Structure):
+    _fields_ = [("flags", ctypes.c_int32), ("A", ctypes.c_void_p), ("lda", ctypes.c_int64),
+                ("Wp", ctypes.c_void_p), ("Kpad", ctypes.c_int32), ("Npad", ctypes.c_int32),
+                ("C", ctypes.c_void_p), ("ldc", ctypes.c_int64), ("M", ctypes.c_int32),
+                ("N", ctypes.c_int32), ("bias", ctypes.c_void_p), ("resid", ctypes.c_void_p),
+                ("ldr", ctypes.c_int64), ("pos", ctypes.c_void_p), ("ldp", ctypes.c_int64),
+                ("P", ctypes.c_int32), ("colsum", ctypes.c_void_p), ("stats_in", ctypes.c_void_p),
+                ("rstats", ctypes.c_void_p), ("rgamma", ctypes.c_void_p),
+                ("rbeta", ctypes.c_void_p), ("stats_out", ctypes.c_void_p),
+                ("ln_width", ctypes.c_int32), ("ln_eps", ctypes.c_float)]
+
+
 # name -> (restype, argtypes); this is the full symbol list of include/evt.h
 _P, _I, _I64, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
 SIGNATURES = {
@@ -55,12 +68,12 @@ SIGNATURES = {
     "evt_query_workspace": (_I, [ctypes.POINTER(evt_vit_desc), _I, ctypes.POINTER(ctypes.c_size_t)]),
     "evt_model_destroy": (_I, [_P]),
     "evt_set_gemm_variant": (_I, [_I]),
-    "evt_pack_weight": (_I, [_I, _P, _I, _I, _P, _I, _I, _P]),
-    "evt_dense": (_I, [_I, _I, _P, _I64, _P, _I, _I, _P, _I64, _I, _I, _P, _P, _I64, _P, _I64, _I,
-                       _P]),
+    "evt_pack_weight": (_I, [_I, _P, _P, _I, _I, _P, _I, _I, _P]),
+    "evt_ln_fold": (_I, [_I, _P, _I, _I, _P, _P, _P, _I, _I, _P, _P, _P]),
+    "evt_dense": (_I, [_I, ctypes.POINTER(evt_dense_args), _P]),
     "evt_attention": (_I, [_I, _P, _I64, _P, _I64, _I, _I, _I, _F, _P]),
     "evt_layernorm": (_I, [_I, _P, _I64, _P, _I64, _P, _P, _I, _I, _F, _P]),
-    "evt_patchify": (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P]),
+    "evt_patchify": (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P]),
 }
 
 _lib = None

@@ -17,7 +17,9 @@ OBJ = os.path.join(HERE, "build_obj")
 SOURCES = ["gemm.hip", "attention.hip", "norm.hip", "capi.cpp"]
 HEADERS = ["common.h", "evt_internal.h", os.path.join("..", "..", "include", "evt.h")]
 ARCH = os.environ.get("EVT_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
+         "-ffp-contract=on"]  # contraction only within one source expression: same result on
+#                                every code path (interior / edge tiles) -> batch-independent bits
 
 
 def _hipcc() -> str:

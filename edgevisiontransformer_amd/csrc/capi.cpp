@@ -1,10 +1,22 @@
 // C ABI of libevt_hip.so (declared in include/evt.h): model plumbing around the HIP kernels.
 //
-// The model handle owns the packed weights (kernel operand layout, zero padded) and one
-// workspace sized for max_batch; evt_vit_forward enqueues the whole ViT forward of reference
-// `modeling/models/vit.py:41-55` on the caller's stream with no host synchronisation.
+// The model handle owns the packed weights (kernel operand layout, zero padded, LayerNorm gamma
+// folded in) and one workspace sized for max_batch; evt_vit_forward enqueues the whole ViT
+// forward of reference `modeling/models/vit.py:41-55` on the caller's stream with no host
+// synchronisation. Per encoder layer (transformer_encoder.py:13-18):
+//
+//   QKV GEMM   A = x (raw stream), epilogue applies LN1 per row        (attention.py:24 + norm.py:12)
+//   attention  fused softmax(q k^T * 64^-0.5) v                        (attention.py:20-34)
+//   out GEMM   + bias + LN1(x) residual -> xm, row stats of xm         (attention.py:35, residual.py:9)
+//   FC1 GEMM   A = xm, epilogue applies LN2 per row, + bias, GELU      (ffn.py:8)
+//   FC2 GEMM   + bias + LN2(xm) residual -> x, row stats of x          (ffn.py:9, residual.py:9)
+//
+// Row statistics (sum, sum of squares) are written by the producing GEMM's epilogue as one partial
+// per 128-column slab (stats slot) with plain stores; consumers sum the slots in a fixed order, so
+// the forward is bitwise reproducible and needs no memsets.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -29,18 +41,25 @@ int hip_fail(hipError_t e, const char* what) {
   return fail(EVT_EHIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-#define EVT_HIP(call, what)                          \
-  do {                                               \
-    hipError_t e__ = (call);                         \
+#define EVT_HIP(call, what)                            \
+  do {                                                 \
+    hipError_t e__ = (call);                           \
     if (e__ != hipSuccess) return hip_fail(e__, what); \
+  } while (0)
+
+#define EVT_RC(x)          \
+  do {                     \
+    int rc__ = (x);        \
+    if (rc__) return rc__; \
   } while (0)
 
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 inline size_t elem_size(int dtype) { return dtype == DT_BF16 ? 2 : 4; }
 
 struct DenseW {  // packed Dense layer
-  void* w = nullptr;      // [npad][kpad] activation dtype
-  float* b = nullptr;     // [npad] fp32, zero padded (may be null)
+  void* w = nullptr;        // [npad][kpad] activation dtype
+  float* b = nullptr;       // [npad] fp32, zero padded (bias, or the LN-fold vector c)
+  float* colsum = nullptr;  // [npad] LN fold: column sums of the packed weights (or null)
   int K = 0, N = 0, kpad = 0, npad = 0;
 };
 
@@ -64,15 +83,16 @@ struct evt_model {
   float *cls = nullptr, *pos = nullptr;
   std::vector<Layer> layers;
   std::vector<void*> allocs;
-  // workspace
-  void* apatch = nullptr;  // [B*P, pd]      (aliases hbuf)
-  float* x = nullptr;      // [B*T, D] fp32 token stream (pre-LN sum)
-  void* y = nullptr;       // [B*T, D]       LN output = GEMM input = residual
-  void* qkv = nullptr;     // [B*T, 3*inner]
-  void* o = nullptr;       // [B*T, inner]
-  void* hbuf = nullptr;    // [B*T, ffn_st]
-  void* t = nullptr;       // [B, D]
-  void* hh = nullptr;      // [B, head_st]
+  // workspace (activation dtype unless noted)
+  void* apatch = nullptr;    // [B*P, pd] patch matrix (aliases hbuf)
+  void* x = nullptr;         // [B*T, D] token stream at layer input / output
+  void* xm = nullptr;        // [B*T, D] token stream between the two sublayers
+  float* sx = nullptr;       // [B*T, nslots, 2] fp32 per-slab (sum, sumsq) of x rows
+  float* sm = nullptr;       // [B*T, nslots, 2] fp32 per-slab (sum, sumsq) of xm rows
+  void* qkv = nullptr;       // [B*T, 3*inner]
+  void* o = nullptr;         // [B*T, inner]
+  void* hbuf = nullptr;      // [B*T, ffn_st]
+  void* hh = nullptr;        // [B, head_st]
   size_t ws_bytes = 0;
 };
 
@@ -81,7 +101,8 @@ namespace {
 int dev_alloc(evt_model* m, void** p, size_t bytes) {
   if (bytes == 0) bytes = 16;
   hipError_t e = hipMalloc(p, bytes);
-  if (e != hipSuccess) return fail(EVT_ENOMEM, std::string("hipMalloc failed: ") + hipGetErrorString(e));
+  if (e != hipSuccess)
+    return fail(EVT_ENOMEM, std::string("hipMalloc failed: ") + hipGetErrorString(e));
   m->allocs.push_back(*p);
   return EVT_OK;
 }
@@ -123,29 +144,34 @@ int validate(const evt_vit_desc* d, Shape* sh) {
   return EVT_OK;
 }
 
-int make_dense(evt_model* m, DenseW* dw, const float* W, const float* b, int K, int N,
-               hipStream_t s) {
+// Pack a Keras [K, N] Dense kernel. With ln_g/ln_b (the LayerNorm in front of it), gamma is folded
+// into the weight rows and b becomes c = beta . W + bias, with the column sums of the packed
+// weights alongside (gemm.hip, "LayerNorm folding").
+int make_dense(evt_model* m, DenseW* dw, const float* W, const float* bias, int K, int N,
+               hipStream_t s, const float* ln_g = nullptr, const float* ln_b = nullptr) {
   const int dt = m->desc.dtype;
   dw->K = K;
   dw->N = N;
   dw->kpad = (int)round_up(K, PAD_K);
   dw->npad = (int)round_up(N, PACK_N);
-  int rc = dev_alloc(m, &dw->w, (size_t)dw->kpad * dw->npad * elem_size(dt));
-  if (rc) return rc;
-  EVT_HIP(pack_weight(dt, W, K, N, dw->w, dw->kpad, dw->npad, s), "pack_weight");
-  if (b) {
-    rc = dev_alloc(m, (void**)&dw->b, (size_t)dw->npad * sizeof(float));
-    if (rc) return rc;
+  EVT_RC(dev_alloc(m, &dw->w, (size_t)dw->kpad * dw->npad * elem_size(dt)));
+  EVT_HIP(pack_weight(dt, W, ln_g, K, N, dw->w, dw->kpad, dw->npad, s), "pack_weight");
+  if (ln_g) {
+    EVT_RC(dev_alloc(m, (void**)&dw->b, (size_t)dw->npad * sizeof(float)));
+    EVT_RC(dev_alloc(m, (void**)&dw->colsum, (size_t)dw->npad * sizeof(float)));
+    EVT_HIP(ln_fold(dt, dw->w, dw->kpad, W, ln_b, bias, K, N, dw->colsum, dw->b, dw->npad, s),
+            "ln_fold");
+  } else if (bias) {
+    EVT_RC(dev_alloc(m, (void**)&dw->b, (size_t)dw->npad * sizeof(float)));
     EVT_HIP(hipMemsetAsync(dw->b, 0, (size_t)dw->npad * sizeof(float), s), "memset bias");
-    EVT_HIP(hipMemcpyAsync(dw->b, b, (size_t)N * sizeof(float), hipMemcpyDeviceToDevice, s),
+    EVT_HIP(hipMemcpyAsync(dw->b, bias, (size_t)N * sizeof(float), hipMemcpyDeviceToDevice, s),
             "copy bias");
   }
   return EVT_OK;
 }
 
 int copy_vec(evt_model* m, float** dst, const float* src, size_t n, hipStream_t s) {
-  int rc = dev_alloc(m, (void**)dst, n * sizeof(float));
-  if (rc) return rc;
+  EVT_RC(dev_alloc(m, (void**)dst, n * sizeof(float)));
   EVT_HIP(hipMemcpyAsync(*dst, src, n * sizeof(float), hipMemcpyDeviceToDevice, s), "copy vec");
   return EVT_OK;
 }
@@ -154,41 +180,61 @@ size_t workspace_bytes(const evt_vit_desc* d, const Shape& sh, int B) {
   const size_t es = elem_size(d->dtype);
   const size_t rows = (size_t)B * sh.T;
   const size_t hb = std::max(rows * sh.max_ffn_st, (size_t)B * sh.P * sh.pd) * es;
-  return rows * sh.D * 4 + rows * sh.D * es + rows * 3 * sh.max_inner * es +
-         rows * sh.max_inner * es + hb + (size_t)B * sh.D * es + (size_t)B * sh.head_st * es +
-         8 * 256;
+  return 2 * rows * sh.D * es + 2 * rows * stats_slots(sh.D) * 2 * sizeof(float) +
+         rows * 3 * sh.max_inner * es +
+         rows * sh.max_inner * es + hb + (size_t)B * sh.head_st * es + 9 * 256;
 }
 
-int dense(const evt_model* m, int flags, const DenseW& w, const void* A, int64_t lda, void* C,
-          int64_t ldc, int M, int N, const void* resid, int64_t ldr, const float* pos,
-          int64_t ldp, int P, hipStream_t s) {
+struct DenseCall {
+  int flags = 0;
+  const void* A = nullptr;
+  int64_t lda = 0;
+  void* C = nullptr;
+  int64_t ldc = 0;
+  int M = 0, N = 0;
+  const void* resid = nullptr;
+  int64_t ldr = 0;
+  const float* pos = nullptr;
+  int64_t ldp = 0;
+  int P = 0;
+  const float* stats_in = nullptr;
+  const float* rstats = nullptr;
+  const float* rgamma = nullptr;
+  const float* rbeta = nullptr;
+  float* stats_out = nullptr;
+};
+
+int dense(const evt_model* m, const DenseW& w, const DenseCall& c, hipStream_t s) {
   GemmParams p{};
-  p.A = A;
-  p.lda = lda;
+  p.A = c.A;
+  p.lda = c.lda;
   p.W = w.w;
   p.ldw = w.kpad;
-  p.C = C;
-  p.ldc = ldc;
-  p.M = M;
-  p.N = N;
+  p.C = c.C;
+  p.ldc = c.ldc;
+  p.M = c.M;
+  p.N = c.N;
   p.K = w.kpad;
   p.ntiles = w.npad / GEMM_BN;
   p.bias = w.b;
-  p.resid = resid;
-  p.ldr = ldr;
-  p.pos = pos;
-  p.ldp = ldp;
-  p.P = P;
-  p.vec_ok = (ldc % 4 == 0) && (ldr % 4 == 0) && (ldp % 4 == 0);
-  EVT_HIP(gemm_launch(m->desc.dtype, flags, p, s), "dense");
+  p.resid = c.resid;
+  p.ldr = c.ldr;
+  p.pos = c.pos;
+  p.ldp = c.ldp;
+  p.P = c.P;
+  p.vec_ok = (c.ldc % 4 == 0) && (c.ldr % 4 == 0) && (c.ldp % 4 == 0);
+  p.colsum = w.colsum;
+  p.stats_in = c.stats_in;
+  p.rstats = c.rstats;
+  p.rgamma = c.rgamma;
+  p.rbeta = c.rbeta;
+  p.stats_out = c.stats_out;
+  p.inv_d = 1.0f / (float)m->desc.dim;
+  p.eps = 1e-5f;  // Keras LayerNormalization(epsilon=1e-5), reference norm.py:6
+  p.nslots = stats_slots(m->desc.dim);
+  EVT_HIP(gemm_launch(m->desc.dtype, c.flags, p, s), "dense");
   return EVT_OK;
 }
-
-#define EVT_RC(x)        \
-  do {                   \
-    int rc__ = (x);      \
-    if (rc__) return rc__; \
-  } while (0)
 
 }  // namespace
 
@@ -250,12 +296,11 @@ int evt_vit_create(const evt_vit_desc* desc, const float* const* w, int n_weight
   m->desc.ffn = m->ffn.data();
   m->sh = sh;
   const int D = desc->dim;
-  int k = 0;
   auto run = [&]() -> int {
     EVT_RC(make_dense(m, &m->patch, w[0], w[1], sh.pd, D, s));
     EVT_RC(copy_vec(m, &m->cls, w[2], D, s));
     EVT_RC(copy_vec(m, &m->pos, w[3], (size_t)sh.T * D, s));
-    k = 4;
+    int k = 4;
     m->layers.resize(desc->depth);
     for (int i = 0; i < desc->depth; ++i) {
       Layer& L = m->layers[i];
@@ -265,11 +310,11 @@ int evt_vit_create(const evt_vit_desc* desc, const float* const* w, int n_weight
       L.ffn_st = (int)round_up(L.ffn, PAD_N);
       EVT_RC(copy_vec(m, &L.ln1_g, w[k + 0], D, s));
       EVT_RC(copy_vec(m, &L.ln1_b, w[k + 1], D, s));
-      EVT_RC(make_dense(m, &L.qkv, w[k + 2], nullptr, D, 3 * L.inner, s));
+      EVT_RC(make_dense(m, &L.qkv, w[k + 2], nullptr, D, 3 * L.inner, s, w[k + 0], w[k + 1]));
       EVT_RC(make_dense(m, &L.out, w[k + 3], w[k + 4], L.inner, D, s));
       EVT_RC(copy_vec(m, &L.ln2_g, w[k + 5], D, s));
       EVT_RC(copy_vec(m, &L.ln2_b, w[k + 6], D, s));
-      EVT_RC(make_dense(m, &L.fc1, w[k + 7], w[k + 8], D, L.ffn, s));
+      EVT_RC(make_dense(m, &L.fc1, w[k + 7], w[k + 8], D, L.ffn, s, w[k + 5], w[k + 6]));
       EVT_RC(make_dense(m, &L.fc2, w[k + 9], w[k + 10], L.ffn, D, s));
       k += 11;
     }
@@ -279,13 +324,15 @@ int evt_vit_create(const evt_vit_desc* desc, const float* const* w, int n_weight
     const int B = desc->max_batch;
     const size_t es = elem_size(desc->dtype);
     const size_t rows = (size_t)B * sh.T;
-    EVT_RC(dev_alloc(m, (void**)&m->x, rows * D * 4));
-    EVT_RC(dev_alloc(m, &m->y, rows * D * es));
+    EVT_RC(dev_alloc(m, &m->x, rows * D * es));
+    EVT_RC(dev_alloc(m, &m->xm, rows * D * es));
+    const size_t stats_bytes = rows * stats_slots(D) * 2 * sizeof(float);
+    EVT_RC(dev_alloc(m, (void**)&m->sx, stats_bytes));
+    EVT_RC(dev_alloc(m, (void**)&m->sm, stats_bytes));
     EVT_RC(dev_alloc(m, &m->qkv, rows * 3 * sh.max_inner * es));
     EVT_RC(dev_alloc(m, &m->o, rows * sh.max_inner * es));
     EVT_RC(dev_alloc(m, &m->hbuf, std::max(rows * sh.max_ffn_st, (size_t)B * sh.P * sh.pd) * es));
     m->apatch = m->hbuf;
-    EVT_RC(dev_alloc(m, &m->t, (size_t)B * D * es));
     EVT_RC(dev_alloc(m, &m->hh, (size_t)B * sh.head_st * es));
     m->ws_bytes = workspace_bytes(desc, sh, B);
     EVT_HIP(hipStreamSynchronize(s), "create sync");
@@ -305,74 +352,128 @@ int evt_vit_create(const evt_vit_desc* desc, const float* const* w, int n_weight
 int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* stream) {
   if (!m || !img || !logits) return fail(EVT_EINVAL, "model, img and logits must be non-null");
   if (B <= 0 || B > m->desc.max_batch)
-    return fail(EVT_EINVAL, "batch must be in [1, max_batch=" + std::to_string(m->desc.max_batch) + "]");
+    return fail(EVT_EINVAL,
+                "batch must be in [1, max_batch=" + std::to_string(m->desc.max_batch) + "]");
   hipStream_t s = (hipStream_t)stream;
   const evt_vit_desc& d = m->desc;
   const Shape& sh = m->sh;
   const int D = d.dim, T = sh.T, rows = B * T, dt = d.dtype;
-  // patch embedding: rearrange -> Dense(D) (+pos, rows 1..P) ; CLS row = cls + pos[0]
+  // patch embedding (vit.py:45-51): rearrange -> Dense(D) + pos, CLS row = cls + pos[0]
   EVT_HIP(patchify_launch(dt, img, B, d.in_chans, d.image_size, d.patch_size, m->apatch, m->x,
-                          m->cls, m->pos, D, s),
+                          m->cls, m->pos, D, m->sx, s),
           "patchify");
-  EVT_RC(dense(m, EPI_BIAS | EPI_POS | EPI_OUT_F32, m->patch, m->apatch, sh.pd, m->x, D, B * sh.P,
-               D, nullptr, 0, m->pos, D, sh.P, s));
+  {
+    DenseCall c;
+    c.flags = EPI_BIAS | EPI_POS | EPI_STATS;
+    c.A = m->apatch; c.lda = sh.pd; c.C = m->x; c.ldc = D; c.M = B * sh.P; c.N = D;
+    c.pos = m->pos; c.ldp = D; c.P = sh.P; c.stats_out = m->sx;
+    EVT_RC(dense(m, m->patch, c, s));
+  }
   const float log2e = 1.4426950408889634f;
   for (const Layer& L : m->layers) {
-    // LayerNorm(Residual(Attention), pre=True): y = LN(x); x = Attn(y) + y
-    EVT_HIP(layernorm_launch(dt, m->x, D, m->y, D, L.ln1_g, L.ln1_b, rows, D, 1e-5f, s), "ln1");
-    EVT_RC(dense(m, 0, L.qkv, m->y, D, m->qkv, 3 * L.inner, rows, 3 * L.inner, nullptr, 0, nullptr,
-                 0, 0, s));
+    {  // LN1-folded QKV (attention.py:24)
+      DenseCall c;
+      c.flags = EPI_LNIN | EPI_BIAS;
+      c.A = m->x; c.lda = D; c.C = m->qkv; c.ldc = 3 * L.inner; c.M = rows; c.N = 3 * L.inner;
+      c.stats_in = m->sx;
+      EVT_RC(dense(m, L.qkv, c, s));
+    }
     AttnParams ap{m->qkv, 3 * L.inner, m->o, L.inner, T, L.heads, B, 0.125f * log2e};
     EVT_HIP(attention_launch(dt, ap, s), "attention");
-    EVT_RC(dense(m, EPI_BIAS | EPI_RESID | EPI_OUT_F32, L.out, m->o, L.inner, m->x, D, rows, D,
-                 m->y, D, nullptr, 0, 0, s));
-    // LayerNorm(Residual(FeedForward), pre=True): y = LN(x); x = FFN(y) + y
-    EVT_HIP(layernorm_launch(dt, m->x, D, m->y, D, L.ln2_g, L.ln2_b, rows, D, 1e-5f, s), "ln2");
-    EVT_RC(dense(m, EPI_BIAS | EPI_GELU, L.fc1, m->y, D, m->hbuf, L.ffn_st, rows, L.ffn_st,
-                 nullptr, 0, nullptr, 0, 0, s));
-    EVT_RC(dense(m, EPI_BIAS | EPI_RESID | EPI_OUT_F32, L.fc2, m->hbuf, L.ffn_st, m->x, D, rows, D,
-                 m->y, D, nullptr, 0, 0, s));
+    {  // out-proj + bias + LN1(x) residual -> xm (+ stats)
+      DenseCall c;
+      c.flags = EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS;
+      c.A = m->o; c.lda = L.inner; c.C = m->xm; c.ldc = D; c.M = rows; c.N = D;
+      c.resid = m->x; c.ldr = D; c.rstats = m->sx; c.rgamma = L.ln1_g; c.rbeta = L.ln1_b;
+      c.stats_out = m->sm;
+      EVT_RC(dense(m, L.out, c, s));
+    }
+    {  // LN2-folded FC1 + GELU (ffn.py:8)
+      DenseCall c;
+      c.flags = EPI_LNIN | EPI_BIAS | EPI_GELU;
+      c.A = m->xm; c.lda = D; c.C = m->hbuf; c.ldc = L.ffn_st; c.M = rows; c.N = L.ffn_st;
+      c.stats_in = m->sm;
+      EVT_RC(dense(m, L.fc1, c, s));
+    }
+    {  // FC2 + bias + LN2(xm) residual -> x (+ stats)
+      DenseCall c;
+      c.flags = EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS;
+      c.A = m->hbuf; c.lda = L.ffn_st; c.C = m->x; c.ldc = D; c.M = rows; c.N = D;
+      c.resid = m->xm; c.ldr = D; c.rstats = m->sm; c.rgamma = L.ln2_g; c.rbeta = L.ln2_b;
+      c.stats_out = m->sx;
+      EVT_RC(dense(m, L.fc2, c, s));
+    }
   }
-  // head on token 0: Dense(M, gelu) -> Dense(C)  (no final LayerNorm in ViT, vit.py:54-55)
-  EVT_HIP(gather_cls_launch(dt, m->x, (int64_t)T * D, B, D, m->t, s), "gather_cls");
-  EVT_RC(dense(m, EPI_BIAS | EPI_GELU, m->head1, m->t, D, m->hh, sh.head_st, B, sh.head_st,
-               nullptr, 0, nullptr, 0, 0, s));
-  EVT_RC(dense(m, EPI_BIAS | EPI_OUT_F32, m->head2, m->hh, sh.head_st, logits, d.num_classes, B,
-               d.num_classes, nullptr, 0, nullptr, 0, 0, s));
+  // head on token 0 (vit.py:54-55; no final LayerNorm): rows b*T of the stream, stride T*D
+  {
+    DenseCall c;
+    c.flags = EPI_BIAS | EPI_GELU;
+    c.A = m->x; c.lda = (int64_t)T * D; c.C = m->hh; c.ldc = sh.head_st; c.M = B; c.N = sh.head_st;
+    EVT_RC(dense(m, m->head1, c, s));
+  }
+  {
+    DenseCall c;
+    c.flags = EPI_BIAS | EPI_OUT_F32;
+    c.A = m->hh; c.lda = sh.head_st; c.C = logits; c.ldc = d.num_classes; c.M = B;
+    c.N = d.num_classes;
+    EVT_RC(dense(m, m->head2, c, s));
+  }
   return EVT_OK;
 }
 
 // ---- op-level entry points --------------------------------------------------------------
 
 int evt_set_gemm_variant(int variant) {
-  if (variant < 0 || variant > 31) return fail(EVT_EINVAL, "variant must be 0..31");
+  if (variant != 0 && variant != 1 && variant != 2 && variant != 6)
+    return fail(EVT_EINVAL, "variant must be 0, 1, 2 or 6");
   gemm_set_variant(variant);
   return EVT_OK;
 }
 
-int evt_pack_weight(int dtype, const float* W, int K, int N, void* Wp, int Kpad, int Npad,
-                    void* stream) {
+int evt_pack_weight(int dtype, const float* W, const float* row_scale, int K, int N, void* Wp,
+                    int Kpad, int Npad, void* stream) {
   if (!W || !Wp || K <= 0 || N <= 0 || Kpad < K || Npad < N || Kpad % PAD_K || Npad % GEMM_BN)
     return fail(EVT_EINVAL, "pack: bad shape (Npad % 128, Kpad % 64, Kpad >= K, Npad >= N)");
-  EVT_HIP(pack_weight(dtype, W, K, N, Wp, Kpad, Npad, (hipStream_t)stream), "pack_weight");
+  EVT_HIP(pack_weight(dtype, W, row_scale, K, N, Wp, Kpad, Npad, (hipStream_t)stream),
+          "pack_weight");
   return EVT_OK;
 }
 
-int evt_dense(int dtype, int flags, const void* A, int64_t lda, const void* Wp, int Kpad, int Npad,
-              void* C, int64_t ldc, int M, int N, const float* bias, const void* resid,
-              int64_t ldr, const float* pos, int64_t ldp, int P, void* stream) {
-  if (!A || !Wp || !C || M < 0 || N <= 0 || N > Npad || Kpad % PAD_K || Npad % GEMM_BN ||
-      lda < Kpad || ldc < N)
+int evt_ln_fold(int dtype, const void* Wp, int Kpad, int Npad, const float* W, const float* beta,
+                const float* bias, int K, int N, float* colsum, float* cvec, void* stream) {
+  if (!Wp || !W || !beta || !colsum || !cvec || K <= 0 || N <= 0 || Kpad < K || Npad < N)
+    return fail(EVT_EINVAL, "ln_fold: bad shape");
+  EVT_HIP(ln_fold(dtype, Wp, Kpad, W, beta, bias, K, N, colsum, cvec, Npad, (hipStream_t)stream),
+          "ln_fold");
+  return EVT_OK;
+}
+
+int evt_dense(int dtype, const evt_dense_args* a, void* stream) {
+  if (!a || !a->A || !a->Wp || !a->C || a->M < 0 || a->N <= 0 || a->N > a->Npad ||
+      a->Kpad % PAD_K || a->Npad % GEMM_BN || a->lda < a->Kpad || a->ldc < a->N)
     return fail(EVT_EINVAL, "dense: bad shape");
-  if ((flags & EPI_BIAS) && !bias) return fail(EVT_EINVAL, "dense: bias flag without bias");
-  if ((flags & EPI_RESID) && (!resid || ldr < N)) return fail(EVT_EINVAL, "dense: bad resid");
-  if ((flags & EPI_POS) && (!pos || P <= 0 || ldp < N)) return fail(EVT_EINVAL, "dense: bad pos");
+  const int f = a->flags;
+  if ((f & EPI_BIAS) && !a->bias) return fail(EVT_EINVAL, "dense: bias flag without bias");
+  if ((f & EPI_RESID) && (!a->resid || a->ldr < a->N)) return fail(EVT_EINVAL, "dense: bad resid");
+  if ((f & EPI_POS) && (!a->pos || a->P <= 0 || a->ldp < a->N))
+    return fail(EVT_EINVAL, "dense: bad pos");
+  if ((f & EPI_LNIN) && (!a->colsum || !a->stats_in || a->ln_width <= 0))
+    return fail(EVT_EINVAL, "dense: LN-in needs colsum, stats_in, ln_width");
+  if ((f & EPI_RESLN) && (!a->rstats || !a->rgamma || !a->rbeta || a->ln_width <= 0))
+    return fail(EVT_EINVAL, "dense: LN residual needs rstats, rgamma, rbeta, ln_width");
+  if ((f & EPI_STATS) && !a->stats_out)
+    return fail(EVT_EINVAL, "dense: stats flag without stats_out");
   GemmParams p{};
-  p.A = A; p.lda = lda; p.W = Wp; p.ldw = Kpad; p.C = C; p.ldc = ldc;
-  p.M = M; p.N = N; p.K = Kpad; p.ntiles = Npad / GEMM_BN;
-  p.bias = bias; p.resid = resid; p.ldr = ldr; p.pos = pos; p.ldp = ldp; p.P = P;
-  p.vec_ok = (ldc % 4 == 0) && (ldr % 4 == 0) && (ldp % 4 == 0);
-  hipError_t e = gemm_launch(dtype, flags, p, (hipStream_t)stream);
+  p.A = a->A; p.lda = a->lda; p.W = a->Wp; p.ldw = a->Kpad; p.C = a->C; p.ldc = a->ldc;
+  p.M = a->M; p.N = a->N; p.K = a->Kpad; p.ntiles = a->Npad / GEMM_BN;
+  p.bias = a->bias; p.resid = a->resid; p.ldr = a->ldr; p.pos = a->pos; p.ldp = a->ldp; p.P = a->P;
+  p.vec_ok = (a->ldc % 4 == 0) && (a->ldr % 4 == 0) && (a->ldp % 4 == 0);
+  p.colsum = a->colsum; p.stats_in = a->stats_in; p.rstats = a->rstats;
+  p.rgamma = a->rgamma; p.rbeta = a->rbeta; p.stats_out = a->stats_out;
+  p.inv_d = a->ln_width > 0 ? 1.0f / (float)a->ln_width : 0.f;
+  p.eps = a->ln_eps;
+  p.nslots = a->ln_width > 0 ? stats_slots(a->ln_width) : 1;
+  hipError_t e = gemm_launch(dtype, f, p, (hipStream_t)stream);
   if (e == hipErrorInvalidValue) return fail(EVT_EINVAL, "dense: unsupported flags/shape");
   EVT_HIP(e, "dense");
   return EVT_OK;
@@ -397,11 +498,12 @@ int evt_layernorm(int dtype, const float* x, int64_t ldx, void* y, int64_t ldy,
   return EVT_OK;
 }
 
-int evt_patchify(int dtype, const float* img, int B, int C, int HW, int ps, void* out, float* x,
-                 const float* cls, const float* pos, int D, void* stream) {
+int evt_patchify(int dtype, const float* img, int B, int C, int HW, int ps, void* out, void* x,
+                 const float* cls, const float* pos, int D, float* stats, void* stream) {
   if (!img || !out || !x || !cls || !pos || B < 0 || C <= 0 || ps <= 0 || HW % ps)
     return fail(EVT_EINVAL, "patchify: bad shape");
-  EVT_HIP(patchify_launch(dtype, img, B, C, HW, ps, out, x, cls, pos, D, (hipStream_t)stream),
+  EVT_HIP(patchify_launch(dtype, img, B, C, HW, ps, out, x, cls, pos, D, stats,
+                          (hipStream_t)stream),
           "patchify");
   return EVT_OK;
 }

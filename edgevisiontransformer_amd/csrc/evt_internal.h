@@ -8,8 +8,17 @@ namespace evt {
 
 enum Dtype : int { DT_F32 = 0, DT_BF16 = 1 };
 
-// Epilogue flags of the token-matrix GEMM.
-enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_POS = 8, EPI_OUT_F32 = 16 };
+// Epilogue flags of the token-matrix GEMM (see gemm.hip header for the LayerNorm folding).
+enum : int {
+  EPI_BIAS = 1,      // + bias[n]
+  EPI_GELU = 2,      // tanh-GELU
+  EPI_RESID = 4,     // + resid[m][n]
+  EPI_POS = 8,       // patch embed: output row remap b*P+t -> b*(P+1)+1+t, + pos[t+1][n]
+  EPI_OUT_F32 = 16,  // fp32 output (else activation dtype)
+  EPI_LNIN = 32,     // A rows are un-normalised: v = r*acc - r*mu*colsum[n] (+ bias = c[n])
+  EPI_RESLN = 64,    // residual is LN(resid): (resid - mu_r) * r_r * rgamma[n] + rbeta[n]
+  EPI_STATS = 128,   // accumulate (sum, sum of squares) of each output row into stats_out
+};
 
 // C[M, N] = epilogue(A[M, K] . W[K, N]) with W pre-packed K-contiguous as Wp[Npad][Kpad].
 // A, resid: activation dtype; C: fp32 when EPI_OUT_F32 else activation dtype.
@@ -24,6 +33,15 @@ struct GemmParams {
   const float* pos;  int64_t ldp;     // EPI_POS: pos[(t+1)*ldp + n], output row remap
   int P;                              // EPI_POS: patches per image
   int vec_ok;                         // all leading dims multiple of 4 -> vector epilogue
+  const float* colsum;                // EPI_LNIN: column sums of the packed (gamma-folded) W
+  const float* stats_in;              // EPI_LNIN: [M][nslots][2] (sum, sumsq) of the A rows
+  const float* rstats;                // EPI_RESLN: [M][nslots][2] stats of the resid rows
+  const float* rgamma;                // EPI_RESLN: LayerNorm gamma / beta of the residual
+  const float* rbeta;
+  float* stats_out;                   // EPI_STATS: [rows][nslots][2] per-slab (sum, sumsq)
+  float inv_d;                        // 1 / LayerNorm width
+  float eps;                          // LayerNorm epsilon (1e-5)
+  int nslots;                         // stats rows are [nslots][2]: per-128-column-slab partials
 };
 constexpr int GEMM_BM = 128;
 constexpr int GEMM_BN = 128;
@@ -33,8 +51,12 @@ constexpr int PAD_N = 64;   // column granularity of activation buffers
 
 hipError_t gemm_launch(int dtype, int flags, const GemmParams& p, hipStream_t s);
 void gemm_set_variant(int v);  // 0 auto, 1 force 128x128 tiles, 2 force 256x256 (bf16)
-hipError_t pack_weight(int dtype, const float* W, int K, int N, void* Wp, int Kpad, int Npad,
-                       hipStream_t s);
+hipError_t pack_weight(int dtype, const float* W, const float* row_scale, int K, int N, void* Wp,
+                       int Kpad, int Npad, hipStream_t s);
+// colsum[n] = sum_k Wp[n][k]; cvec[n] = sum_k beta[k] W[k][n] + bias[n] (bias may be null).
+hipError_t ln_fold(int dtype, const void* Wp, int Kpad, const float* W, const float* beta,
+                   const float* bias, int K, int N, float* colsum, float* cvec, int Npad,
+                   hipStream_t s);
 
 struct AttnParams {
   const void* qkv; int64_t ldq;   // token rows, columns (qkv h d)
@@ -51,13 +73,15 @@ hipError_t layernorm_launch(int dtype, const float* x, int64_t ldx, void* y, int
                             const float* gamma, const float* beta, int rows, int D, float eps,
                             hipStream_t s);
 
-// NCHW fp32 images -> patch matrix [B*P, p*p*C] (p1 p2 c) in activation dtype; also writes
-// x[b*(P+1)] = cls + pos[0] (fp32 token stream).
-hipError_t patchify_launch(int dtype, const float* img, int B, int C, int HW, int ps, void* out,
-                           float* x, const float* cls, const float* pos, int D, hipStream_t s);
+// Number of statistics slots of a LayerNorm of width D: one per 128-column slab of a 256-padded
+// row (both GEMM tile shapes number their slabs n0 / 128).
+__host__ __device__ inline int stats_slots(int D) { return 2 * ((D + 255) / 256); }
 
-// Gather token-0 rows of the fp32 stream into a dense [B, D] activation-dtype matrix.
-hipError_t gather_cls_launch(int dtype, const float* x, int64_t row_stride, int B, int D, void* out,
-                             hipStream_t s);
+// NCHW fp32 images -> patch matrix [B*P, p*p*C] (p1 p2 c) in activation dtype; also writes
+// the CLS token row x[b*(P+1)] = cls + pos[0] (activation dtype, row stride D) and, when stats is
+// non-null, its (sum, sumsq) into slot 0 of stats[b*(P+1)] (other slots zeroed).
+hipError_t patchify_launch(int dtype, const float* img, int B, int C, int HW, int ps, void* out,
+                           void* x, const float* cls, const float* pos, int D, float* stats,
+                           hipStream_t s);
 
 }  // namespace evt

@@ -2,26 +2,45 @@
 //
 // Replaces every tf.keras.layers.Dense on the hot path (reference `modeling/layers/attention.py:17-18`
 // to_qkv / to_out, `modeling/layers/ffn.py:8-9` FC1+gelu / FC2, `modeling/models/vit.py:23,38-39`
-// patch_to_embedding / mlp_head) as one templated MFMA kernel with fused epilogues.
+// patch_to_embedding / mlp_head) with fused epilogues, including the two LayerNorms of every
+// encoder layer (reference `modeling/layers/norm.py:6,12`), which never run as kernels of their
+// own (see "LayerNorm folding" below).
 //
 // Layout. A (activations) is row-major [M][lda]; weights are packed once at model creation to
 // Wp[Npad][Kpad] (K-contiguous, zero padded), so both MFMA operands are 16-byte K-contiguous
-// reads. Per stage the block stages 128 bytes of K for a 128-row A tile and a 128-row W tile
-// into LDS with global_load_lds (async, 16 B/lane), double buffered. The LDS image is
-// row-linear; the bank-conflict swizzle (chunk ^ (row & 7)) is applied to the per-lane SOURCE
-// address and to the ds_read address (glds writes lane-linear).
+// reads. Tiles of A and W are staged into LDS with global_load_lds (async, 16 B/lane); the LDS
+// image is row-linear and the bank-conflict swizzle (chunk ^ (row & 7)) is applied to the
+// per-lane SOURCE address and to the ds_read address (glds writes lane-linear).
 //
-// MFMA. The product is computed transposed, C^T = W . A^T, so that each lane ends up owning 4
-// consecutive output COLUMNS of one row (16x16 C layout: col = lane&15 -> token row m,
-// row = 4*(lane>>4)+j -> feature n): epilogue loads/stores are 8-16 B per lane.
+// MFMA. The product is computed transposed, C^T = W . A^T (16x16 C layout: col = lane&15 ->
+// token row m, row = 4*(lane>>4)+j -> feature n).
 //   bf16: v_mfma_f32_16x16x32_bf16, one 16-B chunk (8 k) per MFMA.
 //   f32 : v_mfma_f32_16x16x4_f32 (exact fp32, the parity path), one 16-B chunk = 4 MFMAs with a
 //         k-permutation shared by both operands.
-// 256 threads = 4 waves in 2(m) x 2(n); each wave owns a 64x64 output tile (4x4 MFMA tiles).
+//
+// Kernels.
+//   gemm_nt_kernel   128x128 tile, 4 waves (64x64 each), 2 blocks/CU; bf16 and f32.
+//   gemm_big_kernel  256x256 tile, 8 waves (128x64 each), 128 KiB LDS, 1 block/CU; bf16, used
+//                    when the problem has >= 256 such tiles (every encoder GEMM at bs >= 64).
+// Both stage the finished accumulator tile through LDS (fp32, XOR-swizzled 512-B rows) and run
+// the epilogue row-major ("epi_rows"): every lane owns 4 consecutive columns of one row and a
+// wave streams 2 full 128-column row segments per instruction, so bias / residual / position
+// loads, output stores and LayerNorm row statistics are all coalesced.
+//
+// LayerNorm folding. The reference sublayer is y = LN(x); out = f(y) + y (norm.py:11-12 +
+// residual.py:9; the residual is the NORMALISED input). With per-row mean mu, rstd r of x and
+// LN(x) = (x - mu) r gamma + beta, the first Dense of the sublayer is
+//     y . W = r (x . W') - r mu s + c,   W' = diag(gamma) W,  s = 1^T W',  c = beta . W (+ bias)
+// so QKV / FC1 consume the raw stream x and apply (mu, r) per row in the epilogue (EPI_LNIN);
+// the residual y is rebuilt element-wise from x in the out-proj / FC2 epilogue (EPI_RESLN), and
+// those epilogues accumulate the row sums (sum x, sum x^2) of the new stream for the next
+// LayerNorm with one atomic pair per row segment (EPI_STATS). No LayerNorm kernel, no fp32
+// stream: the token stream x is kept in the activation dtype.
 //
 // Grid. 1-D, XCD-aware bijective remap so that consecutive logical tiles (same A rows, all N
 // tiles) run on one XCD and share its L2.
 #include <type_traits>
+
 #include "common.h"
 #include "evt_internal.h"
 
@@ -32,7 +51,6 @@ namespace {
 constexpr int ROWB = 128;                       // bytes of K per row per stage
 constexpr int TILE_BYTES = GEMM_BM * ROWB;      // 16 KiB per operand tile
 constexpr int STAGE_BYTES = 2 * TILE_BYTES;     // A + W
-constexpr int BIG_BN_ = 256;
 
 template <typename T> struct Mma;
 template <> struct Mma<bf16> {
@@ -49,49 +67,6 @@ template <> struct Mma<float> {
   }
 };
 
-
-template <int FL>
-__device__ __forceinline__ f32x4 epi_bias(const GemmParams& p, int n, bool full) {
-  // full: the 4 columns are in range and 16-B aligned (always true on interior tiles)
-  f32x4 b4 = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (FL & EPI_BIAS) {
-    if (full) b4 = load4(p.bias + n);
-    else
-      for (int j = 0; j < 4; ++j) b4[j] = (n + j < p.N) ? p.bias[n + j] : 0.f;
-  }
-  return b4;
-}
-
-// v = acc + bias for C[m][n..n+3]; applies gelu / pos (+row remap) / residual and stores.
-template <typename T, int FL>
-__device__ __forceinline__ void epi_store(const GemmParams& p, f32x4 v, int m, int n, bool full) {
-  typedef typename std::conditional<(FL & EPI_OUT_F32) != 0, float, T>::type TO;
-  if (FL & EPI_GELU) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(v[j]);
-  }
-  int64_t orow = m;
-  if (FL & EPI_POS) {
-    const int img = m / p.P, t = m - img * p.P;
-    orow = (int64_t)img * (p.P + 1) + 1 + t;
-    const float* pp = p.pos + (int64_t)(t + 1) * p.ldp + n;
-    if (full) v += load4(pp);
-    else
-      for (int j = 0; j < 4; ++j) v[j] += (n + j < p.N) ? pp[j] : 0.f;
-  }
-  if (FL & EPI_RESID) {
-    const T* rp = (const T*)p.resid + (int64_t)m * p.ldr + n;
-    if (full) v += load4(rp);
-    else
-      for (int j = 0; j < 4; ++j) v[j] += (n + j < p.N) ? to_f32(rp[j]) : 0.f;
-  }
-  TO* cp = (TO*)p.C + orow * p.ldc + n;
-  if (full) store4(cp, v);
-  else
-    for (int j = 0; j < 4; ++j)
-      if (n + j < p.N) cp[j] = from_f32<TO>(v[j]);
-}
-
 // Bijective XCD-aware remap: blocks b and b+8 share an XCD (round-robin dispatch), so give each
 // XCD a contiguous range of logical tiles (tile order: all N tiles of one M block consecutively,
 // so an XCD's L2 keeps the A panel while it sweeps N).
@@ -100,6 +75,171 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
 }
 
+// Load 4 per-column fp32 values (zero past N).
+__device__ __forceinline__ f32x4 col4(const float* v, int n, int N, bool full) {
+  if (full) return load4(v + n);
+  f32x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = (n + j < N) ? v[n + j] : 0.f;
+  return r;
+}
+
+// LayerNorm coefficients of one row from its per-slab partial statistics
+// stats[row][slot][2] = (sum, sumsq), summed over the slots in a fixed order (deterministic).
+__device__ __forceinline__ void ln_coef(const float* stats, int nslots, int64_t row, float inv_d,
+                                        float eps, float& mu, float& r) {
+  const float2* st = (const float2*)(stats + 2 * nslots * row);
+  float s1 = 0.f, s2 = 0.f;
+  for (int j = 0; j < nslots; ++j) {
+    const float2 v = st[j];
+    s1 += v.x;
+    s2 += v.y;
+  }
+  mu = s1 * inv_d;
+  r = rsqrtf(fmaxf(s2 * inv_d - mu * mu, 0.f) + eps);
+}
+
+// Staged-tile addressing: fp32 rows of 512 B (128 columns), 16-B chunk c of row r at
+// c ^ (r & 7): conflict-free for the 16-B fragment writes and the row reads.
+__device__ __forceinline__ int stg_off(int row, int chunk) { return row * 512 + ((chunk ^ (row & 7)) << 4); }
+
+// Broadcast the value held by lane `l0` (lanes 0-31) or `l0 + 1` (lanes 32-63): per-row
+// coefficients of the two rows an iteration covers, with two v_readlane (no LDS traffic).
+__device__ __forceinline__ float row_bcast(float v, int l0, int sub) {
+  const float a = __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l0) ;
+  const float b = __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l0 + 1);
+  return __builtin_bit_cast(float, (int)(sub ? b : a));
+}
+
+// Row-major epilogue over the 32 staged rows [row_lo, row_lo+32) of one wave (2 rows per
+// iteration: lane>>5) of a staged 128-column slab; lane chunk c = lane & 31 holds global columns
+// n .. n+3 (n supplied by the caller: the slab need not be contiguous). Per-row LayerNorm
+// coefficients are computed once per lane (lane c: row row_lo + c) and broadcast with readlane.
+// EPI_STATS: each lane parks its 4-column partial (sum, sumsq) of the stored values in the LDS
+// row it has just consumed; at the end every row's 32 partials are summed in a fixed order and
+// written to stats slot `slot` of that row (no atomics: bitwise reproducible).
+template <typename T, int FL, bool INTERIOR>
+__device__ __forceinline__ void epi_rows_t(const GemmParams& p, EVT_LDS char* stg, int m0, int n,
+                                           int row_lo, int lane, int slot) {
+  typedef typename std::conditional<(FL & EPI_OUT_F32) != 0, float, T>::type TO;
+  constexpr bool interior = INTERIOR;  // interior tiles: no per-row / per-column range checks
+  const int sub = lane >> 5, c = lane & 31;
+  const bool col_ok = interior || n < p.N;
+  const bool full = interior || (p.vec_ok && n + 4 <= p.N);
+  f32x4 bias4 = f32x4{0.f, 0.f, 0.f, 0.f}, cs4 = bias4, g4 = bias4, b4 = bias4;
+  if (col_ok) {
+    if (FL & EPI_BIAS) bias4 = col4(p.bias, n, p.N, full);
+    if (FL & EPI_LNIN) cs4 = col4(p.colsum, n, p.N, full);
+    if (FL & EPI_RESLN) {
+      g4 = col4(p.rgamma, n, p.N, full);
+      b4 = col4(p.rbeta, n, p.N, full);
+    }
+  }
+  // per-row LayerNorm coefficients: lane c (both halves) owns row row_lo + c
+  float in_mu = 0.f, in_r = 0.f, rs_mu = 0.f, rs_r = 0.f;
+  if (FL & (EPI_LNIN | EPI_RESLN)) {
+    const int mr = m0 + row_lo + c;
+    if (interior || mr < p.M) {
+      if (FL & EPI_LNIN) ln_coef(p.stats_in, p.nslots, mr, p.inv_d, p.eps, in_mu, in_r);
+      if (FL & EPI_RESLN) ln_coef(p.rstats, p.nslots, mr, p.inv_d, p.eps, rs_mu, rs_r);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    // two groups of 8 iterations: bounds how many loads the scheduler hoists (VGPR pressure)
+    if (i == 8) __builtin_amdgcn_sched_barrier(0);
+    const int row = row_lo + 2 * i + sub;
+    const int m = m0 + row;
+    const bool ok = col_ok && (interior || m < p.M);
+    f32x4 v = *(const EVT_LDS f32x4*)(stg + stg_off(row, c));
+    int64_t orow = m;
+    if (FL & EPI_LNIN) {
+      const float mu = row_bcast(in_mu, 2 * i, sub), r = row_bcast(in_r, 2 * i, sub);
+      v = v * r - cs4 * (r * mu) + bias4;
+    } else if (FL & EPI_BIAS) {
+      v += bias4;
+    }
+    if (FL & EPI_GELU) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(v[j]);
+    }
+    if (FL & EPI_POS) {
+      const int img = m / p.P, t = m - img * p.P;
+      orow = (int64_t)img * (p.P + 1) + 1 + t;
+      if (ok) v += col4(p.pos + (int64_t)(t + 1) * p.ldp, n, p.N, full);
+    }
+    if (FL & EPI_RESID) {
+      f32x4 rv = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (ok) {
+        const T* rp = (const T*)p.resid + (int64_t)m * p.ldr + n;
+        if (full) rv = load4(rp);
+        else
+          for (int j = 0; j < 4; ++j) rv[j] = (n + j < p.N) ? to_f32(rp[j]) : 0.f;
+      }
+      if (FL & EPI_RESLN) {
+        const float mu = row_bcast(rs_mu, 2 * i, sub), r = row_bcast(rs_r, 2 * i, sub);
+        rv = (rv - mu) * r * g4 + b4;
+      }
+      v += rv;
+    }
+    if (ok) {
+      TO* cp = (TO*)p.C + orow * p.ldc + n;
+      if (full) store4(cp, v);
+      else
+        for (int j = 0; j < 4; ++j)
+          if (n + j < p.N) cp[j] = from_f32<TO>(v[j]);
+    }
+    if (FL & EPI_STATS) {
+      // partial statistics of the values as stored (what the next LayerNorm reads), parked in
+      // the first 512 B of row row_lo + 2i, which both half-waves have already read
+      float s1 = 0.f, s2 = 0.f;
+      if (ok) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float q = (full || n + j < p.N) ? to_f32(from_f32<TO>(v[j])) : 0.f;
+          s1 += q;
+          s2 += q * q;
+        }
+      }
+      *(EVT_LDS f32x2*)(stg + (row_lo + 2 * i) * 512 + sub * 256 + c * 8) = f32x2{s1, s2};
+    }
+  }
+  if (FL & EPI_STATS) {
+    // lane (q = lane & 31, hf = lane >> 5): row row_lo + q, partials [16 hf, 16 hf + 16)
+    const int q = lane & 31, hf = lane >> 5;
+    const EVT_LDS char* src = stg + (row_lo + (q & ~1)) * 512 + (q & 1) * 256 + hf * 128;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4 v = *(const EVT_LDS f32x4*)(src + j * 16);
+      s1 += v[0] + v[2];
+      s2 += v[1] + v[3];
+    }
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    const int m = m0 + row_lo + q;
+    if (hf == 0 && (interior || m < p.M)) {
+      int64_t orow = m;
+      if (FL & EPI_POS) {
+        const int img = m / p.P, t = m - img * p.P;
+        orow = (int64_t)img * (p.P + 1) + 1 + t;
+      }
+      *(f32x2*)(p.stats_out + 2 * (p.nslots * orow + slot)) = f32x2{s1, s2};
+    }
+  }
+}
+
+template <typename T, int FL>
+__device__ __forceinline__ void epi_rows(const GemmParams& p, EVT_LDS char* stg, int m0, int n,
+                                         int row_lo, int lane, int slot, bool interior) {
+  if (interior) epi_rows_t<T, FL, true>(p, stg, m0, n, row_lo, lane, slot);
+  else epi_rows_t<T, FL, false>(p, stg, m0, n, row_lo, lane, slot);
+}
+
+// ---------------------------------------------------------------------------------------------
+// 128x128 tile kernel (bf16 and f32): 256 threads = 4 waves in 2 (m) x 2 (n), 64x64 per wave,
+// 2-stage glds double buffer (64 KiB), two blocks per CU.
+// ---------------------------------------------------------------------------------------------
 template <typename T, int FL>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
@@ -107,32 +247,24 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmParams p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably uniform -> SGPR math
   const int wm = wave & 1, wn = wave >> 1;
-
-  // ---- XCD-aware bijective block remap ----
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = wgid / p.ntiles, tn = wgid - tm * p.ntiles;
   const int m0 = tm * GEMM_BM, n0 = tn * GEMM_BN;
 
-  // ---- staging addresses: wave stages rows [wave*32, wave*32+32) of both tiles ----
+  // ---- staging: wave stages rows [wave*32, wave*32+32) of both tiles ----
   const int srow = lane >> 3, sslot = lane & 7;
   const int64_t lda_b = p.lda * (int64_t)sizeof(T), ldw_b = p.ldw * (int64_t)sizeof(T);
-  const char* a_src[4];
-  const char* w_src[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = wave * 32 + i * 8 + srow;
-    const int gm = min(m0 + row, p.M - 1);
-    const int chunk = sslot ^ srow;  // (row & 7) == srow
-    a_src[i] = (const char*)p.A + gm * lda_b + chunk * 16;
-    w_src[i] = (const char*)p.W + (int64_t)(n0 + row) * ldw_b + chunk * 16;
-  }
+  const int arow0 = m0 + wave * 32 + srow;
+  const char* a_base = (const char*)p.A + ((sslot ^ srow) * 16);
+  const char* w_base = (const char*)p.W + (int64_t)(n0 + wave * 32 + srow) * ldw_b + ((sslot ^ srow) * 16);
   auto stage = [&](int kt, int buf) {
     EVT_LDS char* base = (EVT_LDS char*)smem + buf * STAGE_BYTES;
     const int64_t koff = (int64_t)kt * ROWB;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      glds16(a_src[i] + koff, base + (wave * 32 + i * 8) * ROWB);
-      glds16(w_src[i] + koff, base + TILE_BYTES + (wave * 32 + i * 8) * ROWB);
+      const int gm = min(arow0 + i * 8, p.M - 1);
+      glds16(a_base + gm * lda_b + koff, base + (wave * 32 + i * 8) * ROWB);
+      glds16(w_base + (i * 8) * ldw_b + koff, base + TILE_BYTES + (wave * 32 + i * 8) * ROWB);
     }
   };
 
@@ -168,106 +300,45 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmParams p) {
     }
   }
 
-  // ---- epilogue: lane owns C[m][n..n+3] ----
+  // ---- stage the 128x128 fp32 tile (exactly the 64 KiB of LDS), then row-major epilogue ----
+  __syncthreads();
+  EVT_LDS char* stg = (EVT_LDS char*)smem;
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    const int n = n0 + wn * 64 + nt * 16 + fg * 4;
-    if (n >= p.N) continue;
-    const bool full = p.vec_ok && (n + 4 <= p.N);
-    const f32x4 bias4 = epi_bias<FL>(p, n, full);
+  for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      const int m = m0 + wm * 64 + mt * 16 + frow;
-      if (m < p.M) epi_store<T, FL>(p, acc[nt][mt] + bias4, m, n, full);
+      const int row = wm * 64 + mt * 16 + frow;
+      *(EVT_LDS f32x4*)(stg + stg_off(row, wn * 16 + nt * 4 + fg)) = acc[nt][mt];
     }
-  }
+  __syncthreads();
+  const bool interior = p.vec_ok && (n0 + GEMM_BN <= p.N) && (m0 + GEMM_BM <= p.M);
+  epi_rows<T, FL>(p, stg, m0, n0 + (lane & 31) * 4, wave * 32, lane, n0 / 128, interior);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Large-tile bf16 kernel: 256x256 output tile, BK = 64, 512 threads = 8 waves in 2 (m) x 4 (n),
+// each wave a 128 (m) x 64 (n) sub-tile = 8 x 4 MFMA tiles (128 fp32 accumulators per lane).
+// 128 KiB LDS (2 buffers x {A 32 KiB, W 32 KiB}), one block per CU; one barrier per K-tile.
+// VAR 6 (default): after the barrier, k-step-0 fragments are read, the 8 DMA pieces of the next
+// K-tile are spread between the first 16 MFMAs and the k-step-1 reads between the next 12
+// (sched_group_barrier), so the DMA issue and LDS latency hide under MFMA issue.
+// VAR 0: the same without the explicit issue order (kept for A/B measurements).
+// ---------------------------------------------------------------------------------------------
+constexpr int BIG_BM = 256, BIG_BN = 256;
+constexpr int BIG_TILE = BIG_BM * ROWB;       // 32 KiB per operand
+constexpr int BIG_STAGE = 2 * BIG_TILE;       // 64 KiB per K-tile
 
-int g_gemm_variant = 0;  // 0 auto, 1 128x128, 2 256x256 plain, 3 staggered, 4 pipelined, 5 ring
+int g_gemm_variant = 0;  // 0 auto, 1 force 128x128, 2 256x256 VAR 0, 6 256x256 VAR 6
 
 bool use_big(const GemmParams& p) {
-  if ((p.ntiles * GEMM_BN) % BIG_BN_) return false;
+  if ((p.ntiles * GEMM_BN) % BIG_BN) return false;
   if (g_gemm_variant == 1) return false;
   if (g_gemm_variant >= 2) return true;
   // enough 256x256 tiles to fill the chip at least once
   return (int64_t)((p.M + 255) / 256) * (p.ntiles * GEMM_BN / 256) >= 256;
 }
 
-// ---------------------------------------------------------------------------------------------
-// Large-tile bf16 kernel: 256x256 output tile, BK = 64, 512 threads = 8 waves in 2 (m) x 4 (n),
-// each wave a 128 (m) x 64 (n) sub-tile = 8 x 4 MFMA tiles (128 fp32 accumulators per lane).
-// 128 KiB LDS (2 buffers x {A 32 KiB, W 32 KiB}), one block per CU. The next K-tile's 8
-// global_load_lds per wave are issued at the top of the current tile so a whole tile of MFMAs
-// (64 per wave) covers their latency; both k32 sub-steps' fragments are read up front so the
-// second step's ds_reads overlap the first step's MFMAs.
-// ---------------------------------------------------------------------------------------------
-constexpr int BIG_BM = 256, BIG_BN = 256;
-constexpr int BIG_TILE = BIG_BM * ROWB;       // 32 KiB per operand
-constexpr int BIG_STAGE = 2 * BIG_TILE;       // 64 KiB per K-tile
-
-
-// LDS-staged epilogue of the 256x256 kernels. The accumulator layout gives each lane 4
-// consecutive columns of one row, i.e. 8-16 B per store spread over 16 rows per instruction
-// (store-issue bound: ~32 narrow stores per lane per tile). Instead, after bias/GELU the tile is
-// staged through the (now idle) 128 KiB LDS in two 128-column fp32 halves (XOR-swizzled
-// 512-B rows: conflict-free 16-B writes and reads), and all 8 waves then stream whole rows:
-// residual loads and output stores become fully coalesced 256-512 B row segments.
-template <int FL>
-__device__ __forceinline__ void big_epilogue(const GemmParams& p, f32x4 (&acc)[4][8], char* smem,
-                                             int m0, int n0, int wm, int wn, int lane, int wave) {
-  typedef typename std::conditional<(FL & EPI_OUT_F32) != 0, float, bf16>::type TO;
-  const int frow = lane & 15, fg = lane >> 4;
-  const bool interior = p.vec_ok && (n0 + 256 <= p.N) && (m0 + 256 <= p.M);
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    __builtin_amdgcn_s_barrier();  // previous readers of the staging area are done
-    if ((wn >> 1) == h) {
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int n = n0 + wn * 64 + nt * 16 + fg * 4;
-        const f32x4 bias4 = epi_bias<FL>(p, n, interior || (p.vec_ok && n + 4 <= p.N));
-        const int chunk = (wn & 1) * 16 + nt * 4 + fg;
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt) {
-          const int row = wm * 128 + mt * 16 + frow;
-          f32x4 v = acc[nt][mt] + bias4;
-          if (FL & EPI_GELU) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(v[j]);
-          }
-          *(EVT_LDS f32x4*)((EVT_LDS char*)smem + row * 512 + ((chunk ^ (row & 7)) * 16)) = v;
-        }
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-    const int sub = lane >> 5, c = lane & 31;
-    const int n = n0 + h * 128 + c * 4;
-#pragma unroll 4
-    for (int i = 0; i < 16; ++i) {
-      const int row = wave * 32 + i * 2 + sub;
-      const int m = m0 + row;
-      f32x4 v = *(const EVT_LDS f32x4*)((EVT_LDS char*)smem + row * 512 + ((c ^ (row & 7)) * 16));
-      if (interior) {
-        int64_t orow = m;
-        if (FL & EPI_POS) {
-          const int img = m / p.P, t = m - img * p.P;
-          orow = (int64_t)img * (p.P + 1) + 1 + t;
-          v += load4(p.pos + (int64_t)(t + 1) * p.ldp + n);
-        }
-        if (FL & EPI_RESID) v += load4((const bf16*)p.resid + (int64_t)m * p.ldr + n);
-        store4((TO*)p.C + orow * p.ldc + n, v);
-      } else if (m < p.M && n < p.N) {
-        const bool full = p.vec_ok && (n + 4 <= p.N);
-        // bias was already added; epi_store adds pos/resid and stores (gelu off here)
-        epi_store<bf16, FL & ~EPI_GELU>(p, v, m, n, full);
-      }
-    }
-  }
-}
-
-template <int FL, int VAR>  // VAR 0: plain, 1: staggered wave groups, 2: software-pipelined
+template <int FL, int VAR>
 __global__ __launch_bounds__(512, 2) void gemm_big_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * BIG_STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -279,8 +350,7 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(GemmParams p) {
 
   const int srow = lane >> 3, sslot = lane & 7;
   const int64_t lda_b = p.lda * 2, ldw_b = p.ldw * 2;
-  // Addresses are recomputed per stage (a few VALU ops) instead of held in 16 VGPRs: the
-  // staggered variant needs every register for fragments + accumulators.
+  // Addresses are recomputed per stage (a few VALU ops) instead of held in 16 VGPRs.
   const int arow0 = m0 + wave * 32 + srow;
   const char* a_base = (const char*)p.A + ((sslot ^ srow) * 16);
   const char* w_base = (const char*)p.W + (int64_t)(n0 + wave * 32 + srow) * ldw_b + ((sslot ^ srow) * 16);
@@ -303,28 +373,6 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(GemmParams p) {
 
   const int nk = p.K / 64;
   const int frow = lane & 15, fsw = lane & 7, fg = lane >> 4;
-  auto read_frags = [&](int kt, u32x4 (&a)[2][8], u32x4 (&w)[2][4]) {
-    const EVT_LDS char* As = (const EVT_LDS char*)smem + (kt & 1) * BIG_STAGE;
-    const EVT_LDS char* Ws = As + BIG_TILE;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int coff = ((fg + 4 * ks) ^ fsw) * 16;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-        w[ks][nt] = *(const EVT_LDS u32x4*)(Ws + (wn * 64 + nt * 16 + frow) * ROWB + coff);
-#pragma unroll
-      for (int mt = 0; mt < 8; ++mt)
-        a[ks][mt] = *(const EVT_LDS u32x4*)(As + (wm * 128 + mt * 16 + frow) * ROWB + coff);
-    }
-  };
-  auto mfma_tile = [&](const u32x4 (&a)[2][8], const u32x4 (&w)[2][4]) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt) Mma<bf16>::run(w[ks][nt], a[ks][mt], acc[nt][mt]);
-  };
   auto read_step = [&](int kt, int ks, u32x4 (&a)[8], u32x4 (&w)[4]) {
     const EVT_LDS char* As = (const EVT_LDS char*)smem + (kt & 1) * BIG_STAGE;
     const EVT_LDS char* Ws = As + BIG_TILE;
@@ -343,99 +391,7 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(GemmParams p) {
       for (int mt = 0; mt < 8; ++mt) Mma<bf16>::run(w[nt], a[mt], acc[nt][mt]);
   };
   stage(0, 0);
-  if constexpr (VAR == 2) {
-    // Software pipeline, one barrier per K-tile. Fragments of (tile t, k-step 0) are read during
-    // the previous tile's second k-step, so every MFMA phase starts with its operands in
-    // registers; the DMA for tile t+2 is issued right after the barrier that retires all reads
-    // of its buffer and has 1.5 K-tiles of MFMAs to land. LDS reads and DMA issues are
-    // interleaved between MFMAs with sched_group_barrier (masks: 0x8 MFMA, 0x10 VMEM,
-    // 0x100 DS read).
-    //   A(t): read (t, ks1) frags | 32 MFMA (t, ks0)
-    //   vmcnt(0) lgkmcnt(0) barrier          -> tile t+1 visible, buffer t&1 free
-    //   B(t): DMA t+2 -> buffer t&1 ; read (t+1, ks0) frags | 32 MFMA (t, ks1) ; lgkmcnt(0)
-    u32x4 a0[8], w0[4], a1[8], w1[4];
-    auto phase_a = [&](int kt) {
-      read_step(kt, 1, a1, w1);
-      mfma_step(a0, w0);
-#pragma unroll
-      for (int i = 0; i < 12; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-    };
-    auto sync = [&]() {
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    auto phase_b = [&](int kt, bool dma, bool next) {
-      if (dma) stage(kt + 2, kt & 1);
-      if (next) read_step(kt + 1, 0, a0, w0);
-      mfma_step(a1, w1);
-      if (dma && next) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x010, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 1);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, 16, 1);
-      } else if (next) {
-#pragma unroll
-        for (int i = 0; i < 12; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 1);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, 8, 1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): (t+1, ks0) frags landed (long since)
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (nk > 1) stage(1, 1);
-    read_step(0, 0, a0, w0);
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    int kt = 0;
-    for (; kt + 2 < nk; ++kt) {
-      phase_a(kt);
-      sync();
-      phase_b(kt, true, true);
-    }
-    if (kt + 1 < nk) {  // kt == nk - 2
-      phase_a(kt);
-      sync();
-      phase_b(kt, false, true);
-      ++kt;
-    }
-    // kt == nk - 1: last tile, no barrier needed (no further DMA)
-    read_step(kt, 1, a1, w1);
-    mfma_step(a0, w0);
-    mfma_step(a1, w1);
-  } else if constexpr (VAR == 0) {
-    for (int kt = 0; kt < nk; ++kt) {
-      wait_vmcnt0();
-      __builtin_amdgcn_s_barrier();
-      if (kt + 1 < nk) stage(kt + 1, (kt + 1) & 1);
-      u32x4 a[2][8], w[2][4];
-      read_frags(kt, a, w);
-      __builtin_amdgcn_s_setprio(1);
-      mfma_tile(a, w);
-      __builtin_amdgcn_s_setprio(0);
-    }
-  } else if constexpr (VAR == 6) {
-    // plain structure (one barrier per K-tile, DMA for tile t+1 issued at the top of tile t),
-    // with an explicit issue order: k-step-0 reads, then the 8 DMA pieces spread between the
-    // first 16 MFMAs, the k-step-1 reads between the next 12, then the remaining MFMAs.
+  if constexpr (VAR == 6) {
     auto tile = [&](int kt, bool dma) {
       wait_vmcnt0();
       __builtin_amdgcn_s_barrier();
@@ -446,12 +402,12 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(GemmParams p) {
       read_step(kt, 1, a1, w1);
       mfma_step(a0, w0);
       mfma_step(a1, w1);
-      __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);  // DS read
       if (dma) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // VMEM (glds)
         }
       } else {
         __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
@@ -466,193 +422,43 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(GemmParams p) {
     };
     for (int kt = 0; kt + 1 < nk; ++kt) tile(kt, true);
     tile(nk - 1, false);
-  } else if constexpr (VAR >= 10) {
-    // ABLATION builds (timing only, outputs meaningless): bit0 no DMA in loop, bit1 no LDS
-    // reads in loop, bit2 no MFMA, bit3 no barrier
-    constexpr int ABL = VAR - 10;
-    u32x4 a[2][8], w[2][4];
-    read_frags(0, a, w);
+  } else {
     for (int kt = 0; kt < nk; ++kt) {
       wait_vmcnt0();
-      if constexpr (!(ABL & 8)) __builtin_amdgcn_s_barrier();
-      if constexpr (!(ABL & 1)) { if (kt + 1 < nk) stage(kt + 1, (kt + 1) & 1); }
-      if constexpr (!(ABL & 2)) read_frags(kt, a, w);
-      if constexpr (!(ABL & 4)) mfma_tile(a, w);
-      else {
+      __builtin_amdgcn_s_barrier();
+      if (kt + 1 < nk) stage(kt + 1, (kt + 1) & 1);
+      u32x4 a[8], w[4];
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(a[ks][i]));
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(w[ks][i]));
+      for (int ks = 0; ks < 2; ++ks) {
+        read_step(kt, ks, a, w);
+        mfma_step(a, w);
       }
     }
-  } else {
-    // Two wave groups (waves 0-3 / 4-7: one of each per SIMD) run half a K-tile apart: group 1
-    // executes one extra barrier up front, so while one group's wave issues its LDS reads and
-    // next-tile DMA, its SIMD partner from the other group runs its 64 MFMAs. Every wave drains
-    // its own DMA (vmcnt) and LDS reads (lgkmcnt) before every barrier, so a K-tile is visible to
-    // all waves one barrier after its last DMA was issued, and a buffer is only re-filled one
-    // barrier after its last reader passed.
-    const int grp = __builtin_amdgcn_readfirstlane(tid) >> 8;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (grp) __builtin_amdgcn_s_barrier();
-    for (int kt = 0; kt < nk; ++kt) {
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      u32x4 a[2][8], w[2][4];
-      read_frags(kt, a, w);
-      if (kt + 1 < nk) stage(kt + 1, (kt + 1) & 1);
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_tile(a, w);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (!grp) __builtin_amdgcn_s_barrier();
   }
 
-  big_epilogue<FL>(p, acc, smem, m0, n0, wm, wn, lane, wave);
-}
-
-
-// ---------------------------------------------------------------------------------------------
-// Ring kernel (bf16): 256x256 output tile, 8 waves (2 m x 4 n, 128x64 per wave), K staged in
-// 32-deep slices (64 B per row) through a 5-slot LDS ring (5 x 32 KiB = all 160 KiB), so four
-// slices (up to 128 KiB) of global_load_lds are in flight while one is consumed: the LDS-DMA
-// latency under full load (~1-2 us) is covered by 3 slices (3 x 32 MFMAs per wave) of work.
-// Per slice: issue DMA for slice s+4, counted vmcnt for slice s+1, ONE barrier, then the
-// fragments of slice s+1 are read between the 32 MFMAs of slice s (register double buffer).
-// 64-B rows use the swizzle chunk ^ ((row >> 1) & 3): conflict-free ds_read_b128.
-// ---------------------------------------------------------------------------------------------
-constexpr int RING_SLOTS = 5;
-constexpr int RING_ROWB = 64;
-constexpr int RING_HALF = 256 * RING_ROWB;  // 16 KiB per operand per slice
-constexpr int RING_SLOT = 2 * RING_HALF;    // 32 KiB
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-}
-
-template <int FL>
-__global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[RING_SLOTS * RING_SLOT];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably uniform -> SGPR math
-  const int wm = wave & 1, wn = wave >> 1;
-  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = wgid / p.ntiles, tn = wgid - tm * p.ntiles;
-  const int m0 = tm * BIG_BM, n0 = tn * BIG_BN;
-
-  // staging: wave w owns rows [w*32, w*32+32) of both operands: 2 glds each (16 rows x 64 B)
-  const int srow = lane >> 2, sslot = lane & 3;
-  const int64_t lda_b = p.lda * 2, ldw_b = p.ldw * 2;
-  const int schunk = (sslot ^ ((srow >> 1) & 3)) * 16;
-  const int arow0 = m0 + wave * 32 + srow;
-  const char* a_base = (const char*)p.A + schunk;
-  const char* w_base = (const char*)p.W + (int64_t)(n0 + wave * 32 + srow) * ldw_b + schunk;
-  auto stage = [&](int sl) {
-    EVT_LDS char* base = (EVT_LDS char*)smem + (sl % RING_SLOTS) * RING_SLOT;
-    const int64_t koff = (int64_t)sl * RING_ROWB;
+  // ---- epilogue: two passes staged through the (idle) 128 KiB of LDS; in pass h every wave
+  // hands over its column tiles nt = 2h, 2h+1 (half of its accumulators die per pass) and all 8
+  // waves then stream 32 rows each of the staged 256 x 128 slab. Stats slot of pass h: 2*tn + h.
+  EVT_LDS char* stg = (EVT_LDS char*)smem;
+  const bool interior = p.vec_ok && (n0 + BIG_BN <= p.N) && (m0 + BIG_BM <= p.M);
+  const int c = lane & 31;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int gm = min(arow0 + i * 16, p.M - 1);
-      glds16(a_base + gm * lda_b + koff, base + (wave * 32 + i * 16) * RING_ROWB);
-      glds16(w_base + (i * 16) * ldw_b + koff, base + RING_HALF + (wave * 32 + i * 16) * RING_ROWB);
-    }
-  };
-
-  f32x4 acc[4][8];
+  for (int h = 0; h < 2; ++h) {
+    __builtin_amdgcn_s_barrier();  // previous readers of the staging area are done
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int frow = lane & 15, fg = lane >> 4;
-  const int coff = (fg ^ ((lane >> 1) & 3)) * 16;
-  auto read_slice = [&](int sl, u32x4 (&a)[8], u32x4 (&w)[4]) {
-    const EVT_LDS char* As = (const EVT_LDS char*)smem + (sl % RING_SLOTS) * RING_SLOT;
-    const EVT_LDS char* Ws = As + RING_HALF;
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-      w[nt] = *(const EVT_LDS u32x4*)(Ws + (wn * 64 + nt * 16 + frow) * RING_ROWB + coff);
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt)
-      a[mt] = *(const EVT_LDS u32x4*)(As + (wm * 128 + mt * 16 + frow) * RING_ROWB + coff);
-  };
-  auto mfma_slice = [&](const u32x4 (&a)[8], const u32x4 (&w)[4]) {
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int mt = 0; mt < 8; ++mt) Mma<bf16>::run(w[nt], a[mt], acc[nt][mt]);
-  };
-  auto barrier = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
+      for (int mt = 0; mt < 8; ++mt) {
+        const int row = wm * 128 + mt * 16 + frow;
+        *(EVT_LDS f32x4*)(stg + stg_off(row, wn * 8 + t * 4 + fg)) = acc[2 * h + t][mt];
+      }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  auto wait_ahead = [&](int sl, int ns) {
-    const int ahead = min(sl + 4, ns - 1) - (sl + 1);  // slices issued after s+1
-    if (ahead >= 3) wait_vm<12>();
-    else if (ahead == 2) wait_vm<8>();
-    else if (ahead == 1) wait_vm<4>();
-    else wait_vm<0>();
-  };
-  auto interleave = [&]() {
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  const int ns = p.K / 32;  // even (K % 64 == 0)
-  const int pre = min(4, ns);
-  for (int i = 0; i < pre; ++i) stage(i);
-  if (pre == 4) wait_vm<12>();
-  else wait_vm<0>();
-  barrier();
-  u32x4 a0[8], w0[4], a1[8], w1[4];
-  read_slice(0, a0, w0);
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  // Each slice: DMA s+4 | counted wait for s+1 | barrier | read s+1 between the MFMAs of s.
-  // Unrolled by two so the fragment double buffer keeps static register names.
-  int sl = 0;
-  for (; sl + 2 < ns; sl += 2) {
-    if (sl + 4 < ns) stage(sl + 4);
-    wait_ahead(sl, ns);
-    barrier();
-    read_slice(sl + 1, a1, w1);
-    mfma_slice(a0, w0);
-    interleave();
-    if (sl + 5 < ns) stage(sl + 5);
-    wait_ahead(sl + 1, ns);
-    barrier();
-    read_slice(sl + 2, a0, w0);
-    mfma_slice(a1, w1);
-    interleave();
+    // staged chunk c holds global columns n0 + (c>>3)*64 + h*32 + (c&7)*4 .. +3
+    epi_rows<bf16, FL>(p, stg, m0, n0 + (c >> 3) * 64 + h * 32 + (c & 7) * 4, wave * 32, lane,
+                       2 * tn + h, interior);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
   }
-  // last two slices (sl == ns - 2): nothing further to load
-  wait_vm<0>();
-  barrier();
-  read_slice(sl + 1, a1, w1);
-  mfma_slice(a0, w0);
-  interleave();
-  mfma_slice(a1, w1);
-
-  big_epilogue<FL>(p, acc, smem, m0, n0, wm, wn, lane, wave);
 }
 
 template <int FL>
@@ -663,32 +469,16 @@ hipError_t launch_big(const GemmParams& p, hipStream_t s) {
   const dim3 grid(mtiles * q.ntiles);
   if (g_gemm_variant == 2)
     hipLaunchKernelGGL((gemm_big_kernel<FL, 0>), grid, dim3(512), 0, s, q);
-  else if (g_gemm_variant == 3)
-    hipLaunchKernelGGL((gemm_big_kernel<FL, 1>), grid, dim3(512), 0, s, q);
-  else if (g_gemm_variant == 4)
-    hipLaunchKernelGGL((gemm_big_kernel<FL, 2>), grid, dim3(512), 0, s, q);
-  else if (g_gemm_variant == 5)
-    hipLaunchKernelGGL((gemm_ring_kernel<FL>), grid, dim3(512), 0, s, q);
-  else if (g_gemm_variant >= 10 && FL == 0) {
-    switch (g_gemm_variant) {
-      case 11: hipLaunchKernelGGL((gemm_big_kernel<FL, 11>), grid, dim3(512), 0, s, q); break;
-      case 12: hipLaunchKernelGGL((gemm_big_kernel<FL, 12>), grid, dim3(512), 0, s, q); break;
-      case 13: hipLaunchKernelGGL((gemm_big_kernel<FL, 13>), grid, dim3(512), 0, s, q); break;
-      case 14: hipLaunchKernelGGL((gemm_big_kernel<FL, 14>), grid, dim3(512), 0, s, q); break;
-      case 15: hipLaunchKernelGGL((gemm_big_kernel<FL, 15>), grid, dim3(512), 0, s, q); break;
-      case 19: hipLaunchKernelGGL((gemm_big_kernel<FL, 19>), grid, dim3(512), 0, s, q); break;
-      case 17: hipLaunchKernelGGL((gemm_big_kernel<FL, 17>), grid, dim3(512), 0, s, q); break;
-      default: hipLaunchKernelGGL((gemm_big_kernel<FL, 10>), grid, dim3(512), 0, s, q); break;
-    }
-  }
-  else  // default (0) and 6
+  else
     hipLaunchKernelGGL((gemm_big_kernel<FL, 6>), grid, dim3(512), 0, s, q);
   return hipGetLastError();
 }
 
 template <typename T, int FL>
 hipError_t launch_t(const GemmParams& p, hipStream_t s) {
-  if (std::is_same<T, bf16>::value && use_big(p)) return launch_big<FL>(p, s);
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (use_big(p)) return launch_big<FL>(p, s);
+  }
   const int mtiles = (p.M + GEMM_BM - 1) / GEMM_BM;
   hipLaunchKernelGGL((gemm_nt_kernel<T, FL>), dim3(mtiles * p.ntiles), dim3(256), 0, s, p);
   return hipGetLastError();
@@ -697,33 +487,63 @@ hipError_t launch_t(const GemmParams& p, hipStream_t s) {
 template <typename T>
 hipError_t dispatch(int flags, const GemmParams& p, hipStream_t s) {
   switch (flags) {
-    case 0: return launch_t<T, 0>(p, s);                                        // QKV
-    case EPI_BIAS | EPI_GELU: return launch_t<T, EPI_BIAS | EPI_GELU>(p, s);    // FC1, head1
-    case EPI_BIAS | EPI_RESID | EPI_OUT_F32:                                    // out-proj, FC2
-      return launch_t<T, EPI_BIAS | EPI_RESID | EPI_OUT_F32>(p, s);
-    case EPI_BIAS | EPI_OUT_F32: return launch_t<T, EPI_BIAS | EPI_OUT_F32>(p, s);  // head2
-    case EPI_BIAS | EPI_POS | EPI_OUT_F32:                                      // patch embed
-      return launch_t<T, EPI_BIAS | EPI_POS | EPI_OUT_F32>(p, s);
-    case EPI_BIAS: return launch_t<T, EPI_BIAS>(p, s);
+#define EVT_CASE(F) \
+  case (F): return launch_t<T, (F)>(p, s);
+    EVT_CASE(0)                                              // plain (op-level)
+    EVT_CASE(EPI_BIAS)
+    EVT_CASE(EPI_BIAS | EPI_GELU)                            // head1
+    EVT_CASE(EPI_BIAS | EPI_OUT_F32)                         // head2 (logits)
+    EVT_CASE(EPI_BIAS | EPI_RESID | EPI_OUT_F32)             // op-level residual
+    EVT_CASE(EPI_BIAS | EPI_POS | EPI_OUT_F32)               // op-level patch embed
+    EVT_CASE(EPI_BIAS | EPI_POS | EPI_STATS)                 // patch embed -> stream + stats
+    EVT_CASE(EPI_LNIN | EPI_BIAS)                            // LN1-folded QKV
+    EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_GELU)                 // LN2-folded FC1 + GELU
+    EVT_CASE(EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS)   // out-proj / FC2 + LN residual
+#undef EVT_CASE
     default: return hipErrorInvalidValue;
   }
 }
 
-// Wp[n][k] = W[k][n] (fp32 [K][N] in) converted to T, zero outside [N) x [K).
+// Wp[n][k] = W[k][n] * (scale ? scale[k] : 1) (fp32 [K][N] in) converted to T, zero outside
+// [N) x [K). `scale` folds a LayerNorm gamma into the weight rows.
 template <typename T>
-__global__ void pack_kernel(const float* __restrict__ W, int K, int N, T* __restrict__ Wp, int Kpad,
-                            int Npad) {
+__global__ void pack_kernel(const float* __restrict__ W, const float* __restrict__ scale, int K,
+                            int N, T* __restrict__ Wp, int Kpad, int Npad) {
   __shared__ float tile[32][33];
   const int k0 = blockIdx.x * 32, n0 = blockIdx.y * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 8 rows per pass
   for (int r = ty; r < 32; r += 8) {
     const int k = k0 + r, n = n0 + tx;
-    tile[r][tx] = (k < K && n < N) ? W[(int64_t)k * N + n] : 0.f;
+    tile[r][tx] = (k < K && n < N) ? W[(int64_t)k * N + n] * (scale ? scale[k] : 1.f) : 0.f;
   }
   __syncthreads();
   for (int r = ty; r < 32; r += 8) {
     const int n = n0 + r, k = k0 + tx;
     if (n < Npad && k < Kpad) Wp[(int64_t)n * Kpad + k] = from_f32<T>(tile[tx][r]);
+  }
+}
+
+// LayerNorm-fold vectors: colsum[n] = sum_k Wp[n][k] (of the packed, rounded weights, so that
+// r (x.W') - r mu colsum == r ((x - mu).W') exactly w.r.t. the weights the GEMM uses) and
+// cvec[n] = sum_k beta[k] W[k][n] + bias[n]. One wave per output column n.
+template <typename T>
+__global__ void fold_kernel(const T* __restrict__ Wp, int Kpad, const float* __restrict__ W,
+                            const float* __restrict__ beta, const float* __restrict__ bias, int K,
+                            int N, float* __restrict__ colsum, float* __restrict__ cvec, int Npad) {
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (n >= Npad) return;
+  float s = 0.f, c = 0.f;
+  if (n < N) {
+    for (int k = lane; k < K; k += 64) {
+      s += to_f32(Wp[(int64_t)n * Kpad + k]);
+      c += beta[k] * W[(int64_t)k * N + n];
+    }
+  }
+  s = wave_sum(s);
+  c = wave_sum(c);
+  if (lane == 0) {
+    colsum[n] = s;
+    cvec[n] = (n < N) ? c + (bias ? bias[n] : 0.f) : 0.f;
   }
 }
 
@@ -738,13 +558,28 @@ hipError_t gemm_launch(int dtype, int flags, const GemmParams& p, hipStream_t s)
   return dtype == DT_BF16 ? dispatch<bf16>(flags, p, s) : dispatch<float>(flags, p, s);
 }
 
-hipError_t pack_weight(int dtype, const float* W, int K, int N, void* Wp, int Kpad, int Npad,
-                       hipStream_t s) {
+hipError_t pack_weight(int dtype, const float* W, const float* row_scale, int K, int N, void* Wp,
+                       int Kpad, int Npad, hipStream_t s) {
   dim3 grid((Kpad + 31) / 32, (Npad + 31) / 32);
   if (dtype == DT_BF16)
-    hipLaunchKernelGGL(pack_kernel<bf16>, grid, dim3(256), 0, s, W, K, N, (bf16*)Wp, Kpad, Npad);
+    hipLaunchKernelGGL(pack_kernel<bf16>, grid, dim3(256), 0, s, W, row_scale, K, N, (bf16*)Wp,
+                       Kpad, Npad);
   else
-    hipLaunchKernelGGL(pack_kernel<float>, grid, dim3(256), 0, s, W, K, N, (float*)Wp, Kpad, Npad);
+    hipLaunchKernelGGL(pack_kernel<float>, grid, dim3(256), 0, s, W, row_scale, K, N, (float*)Wp,
+                       Kpad, Npad);
+  return hipGetLastError();
+}
+
+hipError_t ln_fold(int dtype, const void* Wp, int Kpad, const float* W, const float* beta,
+                   const float* bias, int K, int N, float* colsum, float* cvec, int Npad,
+                   hipStream_t s) {
+  dim3 grid((Npad + 3) / 4);
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(fold_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)Wp, Kpad, W, beta,
+                       bias, K, N, colsum, cvec, Npad);
+  else
+    hipLaunchKernelGGL(fold_kernel<float>, grid, dim3(256), 0, s, (const float*)Wp, Kpad, W, beta,
+                       bias, K, N, colsum, cvec, Npad);
   return hipGetLastError();
 }
 

@@ -1,16 +1,17 @@
-// Memory-bound kernels of the ViT forward on gfx950: LayerNorm, patchify (+CLS row), CLS gather.
+// Memory-bound kernels of the ViT forward on gfx950: patchify (+CLS row) and a standalone LayerNorm.
 //
-// LayerNorm replaces Keras LayerNormalization(epsilon=1e-5) of reference
-// `modeling/layers/norm.py:6,12`: population variance over the last axis, fp32 statistics.
-// One wave64 per token row, 16-B loads, the row held in registers (D <= 1024), two-pass mean /
-// variance with butterfly wave reductions; output written in the activation dtype (bf16 feeds the
-// next MFMA GEMM directly and is also that sublayer's residual, reference `residual.py:9`).
+// In the model forward the encoder LayerNorms are folded into the GEMMs (gemm.hip header); the
+// standalone LayerNorm below is the op-level evt_layernorm (Keras LayerNormalization(epsilon),
+// reference `modeling/layers/norm.py:6`): population variance over the last axis, fp32
+// statistics, one wave64 per row, 16-B loads, the row held in registers (D <= 1024), two-pass
+// mean / variance with butterfly wave reductions, output in the activation dtype.
 //
 // patchify replaces the einops Rearrange 'b c (h p1) (w p2) -> b (h w) (p1 p2 c)' of reference
 // `modeling/models/vit.py:31-32,45`: one workgroup per (image, patch-row) stages the
 // [C][ps][W] strip of the NCHW image in LDS with coalesced 16-B loads, then writes the 14 patch
 // vectors of that row coalesced in (p1 p2 c) order. The first strip of each image also writes the
-// CLS token row x[b, 0] = cls + pos[0] (reference vit.py:48-51) into the fp32 token stream.
+// CLS token row x[b, 0] = cls + pos[0] (reference vit.py:48-51) into the token stream, with the
+// row statistics the folded LayerNorm of layer 0 needs.
 #include "common.h"
 #include "evt_internal.h"
 
@@ -60,9 +61,10 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 template <typename TO>
 __global__ __launch_bounds__(256) void patchify_kernel(const float* __restrict__ img, int C, int HW,
                                                        int ps, TO* __restrict__ out,
-                                                       float* __restrict__ x,
+                                                       TO* __restrict__ x,
                                                        const float* __restrict__ cls,
-                                                       const float* __restrict__ pos, int D) {
+                                                       const float* __restrict__ pos, int D,
+                                                       float* __restrict__ stats) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* strip = (float*)smem;
   const int hh = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
@@ -81,19 +83,25 @@ __global__ __launch_bounds__(256) void patchify_kernel(const float* __restrict__
     const int c = f % C, p12 = f / C, p1 = p12 / ps, p2 = p12 - p1 * ps;
     orow[(int64_t)ww * pd + f] = from_f32<TO>(strip[c * per_c + p1 * HW + ww * ps + p2]);
   }
-  if (hh == 0) {
-    float* xr = x + (int64_t)b * (np * np + 1) * D;
-    for (int n = tid; n < D; n += 256) xr[n] = cls[n] + pos[n];
+  if (hh == 0 && tid < 64) {  // one wave writes the CLS row and its LayerNorm statistics
+    const int64_t row = (int64_t)b * (np * np + 1);
+    TO* xr = x + row * D;
+    float s1 = 0.f, s2 = 0.f;
+    for (int n = tid; n < D; n += 64) {
+      const TO v = from_f32<TO>(cls[n] + pos[n]);
+      xr[n] = v;
+      const float q = to_f32(v);
+      s1 += q;
+      s2 += q * q;
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (stats && tid < stats_slots(D)) {
+      float* st = stats + 2 * (stats_slots(D) * row + tid);
+      st[0] = tid == 0 ? s1 : 0.f;
+      st[1] = tid == 0 ? s2 : 0.f;
+    }
   }
-}
-
-template <typename TO>
-__global__ void gather_cls_kernel(const float* __restrict__ x, int64_t stride, int B, int D,
-                                  TO* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * D) return;
-  const int b = i / D, n = i - b * D;
-  out[i] = from_f32<TO>(x[(int64_t)b * stride + n]);
 }
 
 template <typename TO, int NV>
@@ -125,7 +133,8 @@ hipError_t layernorm_launch(int dtype, const float* x, int64_t ldx, void* y, int
 }
 
 hipError_t patchify_launch(int dtype, const float* img, int B, int C, int HW, int ps, void* out,
-                           float* x, const float* cls, const float* pos, int D, hipStream_t s) {
+                           void* x, const float* cls, const float* pos, int D, float* stats,
+                           hipStream_t s) {
   if (B <= 0) return hipSuccess;
   if (HW % ps || (ps * HW) % 4) return hipErrorInvalidValue;
   const size_t lds = (size_t)C * ps * HW * sizeof(float);
@@ -135,26 +144,13 @@ hipError_t patchify_launch(int dtype, const float* img, int B, int C, int HW, in
     hipFuncSetAttribute((const void*)patchify_kernel<bf16>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(patchify_kernel<bf16>, grid, dim3(256), lds, s, img, C, HW, ps, (bf16*)out,
-                       x, cls, pos, D);
+                       (bf16*)x, cls, pos, D, stats);
   } else {
     hipFuncSetAttribute((const void*)patchify_kernel<float>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(patchify_kernel<float>, grid, dim3(256), lds, s, img, C, HW, ps,
-                       (float*)out, x, cls, pos, D);
+                       (float*)out, (float*)x, cls, pos, D, stats);
   }
-  return hipGetLastError();
-}
-
-hipError_t gather_cls_launch(int dtype, const float* x, int64_t row_stride, int B, int D, void* out,
-                             hipStream_t s) {
-  const int n = B * D;
-  if (n <= 0) return hipSuccess;
-  if (dtype == DT_BF16)
-    hipLaunchKernelGGL(gather_cls_kernel<bf16>, dim3((n + 255) / 256), dim3(256), 0, s, x,
-                       row_stride, B, D, (bf16*)out);
-  else
-    hipLaunchKernelGGL(gather_cls_kernel<float>, dim3((n + 255) / 256), dim3(256), 0, s, x,
-                       row_stride, B, D, (float*)out);
   return hipGetLastError();
 }
 

@@ -94,20 +94,55 @@ int evt_model_destroy(evt_model* model);
 /* ---- op-level entry points (one per hot-path kernel; used by the parity tests) ---------- */
 
 /* GEMM tile-shape policy for bf16 (process-wide tuning knob): 0 = automatic (256x256 tiles when
- * the problem fills the chip, else 128x128), 1 = always 128x128, 2 = 256x256 whenever packable. */
+ * the problem has >= 256 of them, else 128x128), 1 = always 128x128, 2 / 6 = 256x256 tiles with
+ * the plain / interleaved main loop whenever the packed width allows. */
 int evt_set_gemm_variant(int variant);
 
-/* Pack a Keras [K, N] fp32 kernel into the GEMM operand layout Wp[Npad][Kpad] (dtype),
- * zero padded. Npad % 128 == 0, Kpad % 64 == 0. */
-int evt_pack_weight(int dtype, const float* W, int K, int N, void* Wp, int Kpad, int Npad,
-                    void* stream);
+/* Pack a Keras [K, N] fp32 kernel into the GEMM operand layout Wp[Npad][Kpad] (dtype), zero
+ * padded, optionally scaling row k by row_scale[k] (a LayerNorm gamma folded into the weights;
+ * NULL = no scaling). Npad % 128 == 0, Kpad % 64 == 0. */
+int evt_pack_weight(int dtype, const float* W, const float* row_scale, int K, int N, void* Wp,
+                    int Kpad, int Npad, void* stream);
 
-/* Dense layer on the token matrix: C = epi(A[M, K] . W) (reference tf.keras.layers.Dense).
- * flags: 1 bias, 2 gelu (tanh), 4 residual add (resid, activation dtype), 8 patch-embed
- * (row remap + pos add), 16 fp32 output. Supported combinations: 0, 3, 21, 17, 25, 1. */
-int evt_dense(int dtype, int flags, const void* A, int64_t lda, const void* Wp, int Kpad, int Npad,
-              void* C, int64_t ldc, int M, int N, const float* bias, const void* resid,
-              int64_t ldr, const float* pos, int64_t ldp, int P, void* stream);
+/* LayerNorm-fold vectors of a packed weight: colsum[n] = sum_k Wp[n][k] and
+ * cvec[n] = sum_k beta[k] W[k][n] + bias[n] (bias may be NULL); arrays of length Npad. */
+int evt_ln_fold(int dtype, const void* Wp, int Kpad, int Npad, const float* W, const float* beta,
+                const float* bias, int K, int N, float* colsum, float* cvec, void* stream);
+
+/* Epilogue flags of evt_dense (combinable as listed under evt_dense). */
+#define EVT_EPI_BIAS 1     /* + bias[n] */
+#define EVT_EPI_GELU 2     /* tanh-GELU (activation.py:13-15) */
+#define EVT_EPI_RESID 4    /* + resid[m][n] (residual.py:9) */
+#define EVT_EPI_POS 8      /* patch embed: row b*P+t -> b*(P+1)+1+t, + pos[t+1][n] (vit.py:45-51) */
+#define EVT_EPI_OUT_F32 16 /* fp32 output (else activation dtype) */
+#define EVT_EPI_LNIN 32    /* A rows un-normalised: r*acc - r*mu*colsum[n] (+ bias = cvec) */
+#define EVT_EPI_RESLN 64   /* residual is LN(resid) with rstats / rgamma / rbeta (norm.py:12) */
+#define EVT_EPI_STATS 128  /* write per-slab (sum, sumsq) of each stored row into stats_out */
+/* LayerNorm row statistics layout: float stats[rows][S][2], S = 2 * ceil(ln_width / 256) slots
+ * (one per 128-column slab); a row's (sum, sumsq) is the sum over its S slots. */
+
+typedef struct evt_dense_args {
+  int32_t flags;
+  const void* A;   int64_t lda;     /* [M, Kpad] activation dtype */
+  const void* Wp;  int32_t Kpad;  int32_t Npad;
+  void* C;         int64_t ldc;     /* [M, N] (fp32 with EVT_EPI_OUT_F32) */
+  int32_t M, N;
+  const float* bias;                /* >= N floats */
+  const void* resid; int64_t ldr;   /* activation dtype */
+  const float* pos;  int64_t ldp;  int32_t P;
+  const float* colsum;              /* EVT_EPI_LNIN */
+  const float* stats_in;            /* EVT_EPI_LNIN: [M][S][2] slot statistics of the A rows */
+  const float* rstats;              /* EVT_EPI_RESLN: [M][S][2] slot statistics of resid rows */
+  const float* rgamma; const float* rbeta;
+  float* stats_out;                 /* EVT_EPI_STATS: [rows][S][2], this call's slots written */
+  int32_t ln_width;                 /* LayerNorm width (D) for the stats */
+  float ln_eps;                     /* LayerNorm epsilon (1e-5 in the reference) */
+} evt_dense_args;
+
+/* Dense layer on the token matrix: C = epi(A . W) (reference tf.keras.layers.Dense), one of the
+ * flag sets 0, 1, 3, 17, 21, 25, 137 (patch embed -> stream), 33 (LN-folded QKV),
+ * 35 (LN-folded FC1 + GELU), 197 (out-proj / FC2 + LN residual + stats). */
+int evt_dense(int dtype, const evt_dense_args* args, void* stream);
 
 /* Multi-head attention core (attention.py:20-34): qkv [B*N, ldq] with columns (qkv h d), head
  * size 64 -> out [B*N, ldo] columns (h d). N <= 256. */
@@ -119,9 +154,11 @@ int evt_layernorm(int dtype, const float* x, int64_t ldx, void* y, int64_t ldy,
                   const float* gamma, const float* beta, int rows, int D, float eps, void* stream);
 
 /* Rearrange 'b c (h p1) (w p2) -> b (h w) (p1 p2 c)' (vit.py:31-32) of fp32 NCHW images into
- * out [B*P, p*p*C] (dtype); also writes x[b*(P+1)*D + n] = cls[n] + pos[n] (vit.py:48-51). */
-int evt_patchify(int dtype, const float* img, int B, int C, int HW, int ps, void* out, float* x,
-                 const float* cls, const float* pos, int D, void* stream);
+ * out [B*P, p*p*C] (dtype); also writes the CLS row x[b*(P+1)*D + n] = cls[n] + pos[n] (dtype,
+ * vit.py:48-51) and, if stats != NULL, its (sum, sumsq) into slot 0 of stats[b*(P+1)] (the
+ * other S-1 slots of that row zeroed; S from the LayerNorm width D as above). */
+int evt_patchify(int dtype, const float* img, int B, int C, int HW, int ps, void* out, void* x,
+                 const float* cls, const float* pos, int D, float* stats, void* stream);
 
 #ifdef __cplusplus
 }

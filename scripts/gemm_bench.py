@@ -26,7 +26,7 @@ for name, (K, N, fl) in shapes.items():
     W = torch.randn((K, N), generator=g, device="cuda") / K ** 0.5
     npad = (N + 255) // 256 * 256
     wp = torch.empty((npad, K), dtype=torch.bfloat16, device="cuda")
-    _lib.check(lib.evt_pack_weight(1, P(W), K, N, P(wp), K, npad, S()))
+    _lib.check(lib.evt_pack_weight(1, P(W), ctypes.c_void_p(0), K, N, P(wp), K, npad, S()))
     bias = torch.randn(npad, generator=g, device="cuda") * 0.1
     R = torch.randn((M, N), generator=g, device="cuda").bfloat16()
     outs = {}
@@ -34,9 +34,12 @@ for name, (K, N, fl) in shapes.items():
         outs[v] = torch.empty((M, N), dtype=torch.float32 if fl & 16 else torch.bfloat16, device="cuda")
     def run(v):
         lib.evt_set_gemm_variant(v)
-        _lib.check(lib.evt_dense(1, fl, P(A), K, P(wp), K, npad, P(outs[v]), N, M, N, P(bias),
-                                 P(R) if fl & 4 else ctypes.c_void_p(0), N if fl & 4 else 0,
-                                 ctypes.c_void_p(0), 0, 0, S()))
+        a = _lib.evt_dense_args()
+        a.flags, a.A, a.lda, a.Wp, a.Kpad, a.Npad = fl, A.data_ptr(), K, wp.data_ptr(), K, npad
+        a.C, a.ldc, a.M, a.N, a.bias = outs[v].data_ptr(), N, M, N, bias.data_ptr()
+        if fl & 4:
+            a.resid, a.ldr = R.data_ptr(), N
+        _lib.check(lib.evt_dense(1, ctypes.byref(a), S()))
     times = {v: [] for v in VARS}
     for v in VARS:
         run(v)

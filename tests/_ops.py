@@ -22,27 +22,45 @@ def round_up(x, m):
     return (x + m - 1) // m * m
 
 
-def pack(W: torch.Tensor, dtype: str) -> tuple:
-    """Keras [K, N] fp32 (device) -> packed [Npad][Kpad]."""
+def pack(W: torch.Tensor, dtype: str, row_scale: torch.Tensor = None) -> tuple:
+    """Keras [K, N] fp32 (device) -> packed [Npad][Kpad] (optionally rows scaled by gamma)."""
     K, N = W.shape
     kpad, npad = round_up(K, 64), round_up(N, 256)
     wp = torch.empty((npad, kpad), dtype=TDT[dtype], device=W.device)
-    _lib.check(_lib.load_library().evt_pack_weight(_lib.DTYPE[dtype], _p(W.contiguous()), K, N,
-                                                    _p(wp), kpad, npad, _s()))
+    _lib.check(_lib.load_library().evt_pack_weight(_lib.DTYPE[dtype], _p(W.contiguous()),
+                                                    _p(row_scale), K, N, _p(wp), kpad, npad, _s()))
     return wp, kpad, npad
 
 
+def ln_fold(dtype, wp, kpad, npad, W, beta, bias=None):
+    K, N = W.shape
+    colsum = torch.empty(npad, device=W.device)
+    cvec = torch.empty(npad, device=W.device)
+    _lib.check(_lib.load_library().evt_ln_fold(_lib.DTYPE[dtype], _p(wp), kpad, npad,
+                                                _p(W.contiguous()), _p(beta), _p(bias), K, N,
+                                                _p(colsum), _p(cvec), _s()))
+    return colsum, cvec
+
+
 def dense(dtype, flags, A, wp, kpad, npad, M, N, ldc=None, bias=None, resid=None, pos=None, P=0,
-          C=None):
+          C=None, colsum=None, stats_in=None, rstats=None, rgamma=None, rbeta=None,
+          stats_out=None, ln_width=0, ln_eps=1e-5):
     out_f32 = bool(flags & _lib.EPI_OUT_F32)
     ldc = ldc or N
     if C is None:
         rows = M if not (flags & _lib.EPI_POS) else (M // P) * (P + 1)
         C = torch.zeros((rows, ldc), dtype=torch.float32 if out_f32 else TDT[dtype], device=A.device)
-    _lib.check(_lib.load_library().evt_dense(
-        _lib.DTYPE[dtype], flags, _p(A), A.stride(0), _p(wp), kpad, npad, _p(C), ldc, M, N,
-        _p(bias), _p(resid), resid.stride(0) if resid is not None else 0, _p(pos),
-        pos.stride(0) if pos is not None else 0, P, _s()))
+    a = _lib.evt_dense_args()
+    a.flags, a.A, a.lda, a.Wp, a.Kpad, a.Npad = flags, A.data_ptr(), A.stride(0), wp.data_ptr(), kpad, npad
+    a.C, a.ldc, a.M, a.N = C.data_ptr(), ldc, M, N
+    for name, t in (("bias", bias), ("resid", resid), ("pos", pos), ("colsum", colsum),
+                    ("stats_in", stats_in), ("rstats", rstats), ("rgamma", rgamma),
+                    ("rbeta", rbeta), ("stats_out", stats_out)):
+        setattr(a, name, t.data_ptr() if t is not None else None)
+    a.ldr = resid.stride(0) if resid is not None else 0
+    a.ldp = pos.stride(0) if pos is not None else 0
+    a.P, a.ln_width, a.ln_eps = P, ln_width, ln_eps
+    _lib.check(_lib.load_library().evt_dense(_lib.DTYPE[dtype], ctypes.byref(a), _s()))
     return C
 
 
@@ -67,7 +85,8 @@ def patchify(dtype, img, ps, cls, pos, D):
     B, C, HW, _ = img.shape
     P = (HW // ps) ** 2
     out = torch.empty((B * P, ps * ps * C), dtype=TDT[dtype], device=img.device)
-    x = torch.zeros((B * (P + 1), D), dtype=torch.float32, device=img.device)
+    x = torch.zeros((B * (P + 1), D), dtype=TDT[dtype], device=img.device)
+    stats = torch.full((B * (P + 1), 2 * ((D + 255) // 256), 2), -1.0, device=img.device)
     _lib.check(_lib.load_library().evt_patchify(_lib.DTYPE[dtype], _p(img), B, C, HW, ps, _p(out),
-                                                _p(x), _p(cls), _p(pos), D, _s()))
-    return out, x
+                                                _p(x), _p(cls), _p(pos), D, _p(stats), _s()))
+    return out, x, stats

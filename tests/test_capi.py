@@ -27,7 +27,7 @@ def lib():
 def test_header_and_binding_agree():
     from edgevisiontransformer_amd import _lib
     assert _declared() == sorted(_lib.SIGNATURES)
-    assert len(_declared()) == 13
+    assert len(_declared()) == 14
 
 
 def test_every_declared_symbol_is_exported(lib):
@@ -60,4 +60,5 @@ def test_op_entry_points_validate_before_launch(lib):
     from edgevisiontransformer_amd import _lib
     assert lib.evt_attention(1, None, 0, None, 0, 1, 197, 3, 0.125, None) == _lib.EVT_EINVAL
     assert lib.evt_layernorm(1, None, 0, None, 0, None, None, 1, 7, 1e-5, None) == _lib.EVT_EINVAL
-    assert lib.evt_pack_weight(1, None, 1, 1, None, 64, 128, None) == _lib.EVT_EINVAL
+    assert lib.evt_pack_weight(1, None, None, 1, 1, None, 64, 128, None) == _lib.EVT_EINVAL
+    assert lib.evt_dense(1, None, None) == _lib.EVT_EINVAL

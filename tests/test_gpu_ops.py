@@ -152,10 +152,101 @@ def test_patchify(gpu, dtype):
     B, C, HW, ps, D = 2, 3, 224, 16, 192
     img = _rand((B, C, HW, HW), 31).float()
     cls, pos = _rand((D,), 32).float(), _rand((197, D), 33).float()
-    out, x = _ops.patchify(dtype, img.to(gpu), ps, cls.to(gpu), pos.to(gpu), D)
+    out, x, stats = _ops.patchify(dtype, img.to(gpu), ps, cls.to(gpu), pos.to(gpu), D)
     torch.cuda.synchronize()
     ref = vit_ref.patchify_nchw(img.numpy(), ps).reshape(B * 196, -1)
     exp = torch.from_numpy(ref).to(_ops.TDT[dtype])
     assert torch.equal(out.cpu(), exp), "patchify is a pure permutation: must be bit-exact"
     xr = x.cpu().reshape(B, 197, D)
-    assert torch.equal(xr[:, 0], (cls + pos[0]).expand(B, D))
+    cls_row = (cls + pos[0]).to(_ops.TDT[dtype])
+    assert torch.equal(xr[:, 0], cls_row.expand(B, D))
+    q = cls_row.double()
+    st = stats.cpu().reshape(B, 197, -1, 2)[:, 0].double()
+    torch.testing.assert_close(st[:, 0, 0], q.sum().expand(B), rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(st[:, 0, 1], (q * q).sum().expand(B), rtol=1e-5, atol=1e-4)
+    assert torch.all(st[:, 1:] == 0)
+
+
+def _ln64(x, g, b, eps=1e-5):
+    mu = x.mean(-1, keepdim=True)
+    var = ((x - mu) ** 2).mean(-1, keepdim=True)
+    return (x - mu) / torch.sqrt(var + eps) * g + b
+
+
+def _nslots(D):
+    return 2 * ((D + 255) // 256)
+
+
+def _stats32(xq):
+    """[rows][S][2] slot statistics with the whole row in slot 0 (include/evt.h layout)."""
+    S = _nslots(xq.shape[-1])
+    st = torch.zeros((xq.shape[0], S, 2), dtype=torch.float32)
+    st[:, 0, 0], st[:, 0, 1] = xq.sum(-1).float(), (xq * xq).sum(-1).float()
+    return st
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("variant", [1, 2, 0])
+@pytest.mark.parametrize("M,D,N,gelu", [(300, 768, 2304, False), (600, 384, 1536, True),
+                                        (197, 192, 537, True)])
+def test_dense_layernorm_folded_input(gpu, dtype, variant, M, D, N, gelu):
+    """QKV / FC1 as run in the model: A = raw stream x, LayerNorm applied per row in the epilogue
+    from (sum, sumsq) statistics, gamma folded into the packed weights (gemm.hip header)."""
+    x64 = _rand((M, D), 41, 1.3) + 0.3
+    g64, be64 = 1.0 + _rand((D,), 42, 0.1), _rand((D,), 43, 0.1)
+    W64, bias64 = _rand((D, N), 44, 1 / math.sqrt(D)), _rand((N,), 45, 0.05)
+    xq = _q(x64, dtype)
+    W = W64.float().to(gpu)
+    g, be, bias = g64.float().to(gpu), be64.float().to(gpu), bias64.float().to(gpu)
+    wp, kpad, npad = _ops.pack(W, dtype, row_scale=g)
+    colsum, cvec = _ops.ln_fold(dtype, wp, kpad, npad, W, be, bias)
+    flags = _lib.EPI_LNIN | _lib.EPI_BIAS | (_lib.EPI_GELU if gelu else 0)
+    lib = _lib.load_library()
+    lib.evt_set_gemm_variant(variant)
+    try:
+        C = _ops.dense(dtype, flags, xq.to(_ops.TDT[dtype]).to(gpu), wp, kpad, npad, M, N,
+                       bias=cvec, colsum=colsum, stats_in=_stats32(xq).to(gpu), ln_width=D)
+        torch.cuda.synchronize()
+    finally:
+        lib.evt_set_gemm_variant(0)
+    ref = _ln64(xq, g64.float().double(), be64.float().double()) @ W64.float().double() \
+        + bias64.float().double()
+    if gelu:
+        ref = _gelu(ref)
+    tol = dict(rtol=2.5e-2, atol=2.5e-2) if dtype == "bf16" else dict(rtol=2e-4, atol=2e-4)
+    torch.testing.assert_close(C.double().cpu(), ref, **tol)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("variant", [1, 2, 0])
+@pytest.mark.parametrize("M,K,D", [(300, 768, 768), (513, 3072, 384), (197, 576, 192)])
+def test_dense_layernorm_residual_and_stats(gpu, dtype, variant, M, K, D):
+    """out-proj / FC2 as run in the model: + bias + LN(resid) residual (the reference's quirk:
+    the residual is the normalised input), storing the new stream and its row statistics."""
+    A64, W64, b64 = _rand((M, K), 51), _rand((K, D), 52, 1 / math.sqrt(K)), _rand((D,), 53, 0.1)
+    x64 = _rand((M, D), 54, 1.1) - 0.2
+    g64, be64 = 1.0 + _rand((D,), 55, 0.1), _rand((D,), 56, 0.1)
+    Aq, xq = _q(A64, dtype), _q(x64, dtype)
+    wp, kpad, npad = _ops.pack(W64.float().to(gpu), dtype)
+    bias = torch.zeros(npad, device=gpu)
+    bias[:D] = b64.float().to(gpu)
+    stats_out = torch.full((M, _nslots(D), 2), float("nan"), device=gpu)
+    lib = _lib.load_library()
+    lib.evt_set_gemm_variant(variant)
+    try:
+        C = _ops.dense(dtype, _lib.EPI_BIAS | _lib.EPI_RESID | _lib.EPI_RESLN | _lib.EPI_STATS,
+                       Aq.to(_ops.TDT[dtype]).to(gpu), wp, kpad, npad, M, D, bias=bias,
+                       resid=xq.to(_ops.TDT[dtype]).to(gpu), rstats=_stats32(xq).to(gpu),
+                       rgamma=g64.float().to(gpu), rbeta=be64.float().to(gpu),
+                       stats_out=stats_out, ln_width=D)
+        torch.cuda.synchronize()
+    finally:
+        lib.evt_set_gemm_variant(0)
+    ref = Aq @ _q(W64.float().double(), dtype) + b64.float().double() \
+        + _ln64(xq, g64.float().double(), be64.float().double())
+    tol = dict(rtol=2e-2, atol=2e-2) if dtype == "bf16" else dict(rtol=1e-4, atol=1e-4)
+    got = C.double().cpu()
+    torch.testing.assert_close(got, ref, **tol)
+    # statistics are of the values as stored
+    torch.testing.assert_close(stats_out.double().cpu().sum(1), _stats32(got).double().sum(1),
+                               rtol=1e-4, atol=1e-2)
