@@ -223,6 +223,9 @@ int dense(const evt_model* m, const DenseW& w, const DenseCall& c, hipStream_t s
   p.ldp = c.ldp;
   p.P = c.P;
   p.vec_ok = (c.ldc % 4 == 0) && (c.ldr % 4 == 0) && (c.ldp % 4 == 0);
+  if (p.vec_ok && c.ldc % 8 == 0 && c.ldr % 8 == 0 && c.ldp % 8 == 0 &&
+      (((uintptr_t)c.C | (uintptr_t)c.resid) & 15) == 0)
+    p.vec_ok = 2;
   p.colsum = w.colsum;
   p.stats_in = c.stats_in;
   p.rstats = c.rstats;
@@ -468,6 +471,9 @@ int evt_dense(int dtype, const evt_dense_args* a, void* stream) {
   p.M = a->M; p.N = a->N; p.K = a->Kpad; p.ntiles = a->Npad / GEMM_BN;
   p.bias = a->bias; p.resid = a->resid; p.ldr = a->ldr; p.pos = a->pos; p.ldp = a->ldp; p.P = a->P;
   p.vec_ok = (a->ldc % 4 == 0) && (a->ldr % 4 == 0) && (a->ldp % 4 == 0);
+  if (p.vec_ok && a->ldc % 8 == 0 && a->ldr % 8 == 0 && a->ldp % 8 == 0 &&
+      (((uintptr_t)a->C | (uintptr_t)a->resid) & 15) == 0)
+    p.vec_ok = 2;
   p.colsum = a->colsum; p.stats_in = a->stats_in; p.rstats = a->rstats;
   p.rgamma = a->rgamma; p.rbeta = a->rbeta; p.stats_out = a->stats_out;
   p.inv_d = a->ln_width > 0 ? 1.0f / (float)a->ln_width : 0.f;

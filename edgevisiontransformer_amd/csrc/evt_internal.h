@@ -32,7 +32,8 @@ struct GemmParams {
   const void* resid; int64_t ldr;     // residual (activation dtype) or null
   const float* pos;  int64_t ldp;     // EPI_POS: pos[(t+1)*ldp + n], output row remap
   int P;                              // EPI_POS: patches per image
-  int vec_ok;                         // all leading dims multiple of 4 -> vector epilogue
+  int vec_ok;                         // 1: leading dims multiple of 4 (vector epilogue);
+                                      // 2: multiple of 8 (16-B bf16 stores)
   const float* colsum;                // EPI_LNIN: column sums of the packed (gamma-folded) W
   const float* stats_in;              // EPI_LNIN: [M][nslots][2] (sum, sumsq) of the A rows
   const float* rstats;                // EPI_RESLN: [M][nslots][2] stats of the resid rows

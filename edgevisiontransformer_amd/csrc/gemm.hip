@@ -106,9 +106,9 @@ __device__ __forceinline__ int stg_off(int row, int chunk) { return row * 512 + 
 // Broadcast the value held by lane `l0` (lanes 0-31) or `l0 + 1` (lanes 32-63): per-row
 // coefficients of the two rows an iteration covers, with two v_readlane (no LDS traffic).
 __device__ __forceinline__ float row_bcast(float v, int l0, int sub) {
-  const float a = __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l0) ;
-  const float b = __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l0 + 1);
-  return __builtin_bit_cast(float, (int)(sub ? b : a));
+  const int a = __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l0);
+  const int b = __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l0 + 1);
+  return __builtin_bit_cast(float, sub ? b : a);
 }
 
 // Row-major epilogue over the 32 staged rows [row_lo, row_lo+32) of one wave (2 rows per
@@ -229,11 +229,167 @@ __device__ __forceinline__ void epi_rows_t(const GemmParams& p, EVT_LDS char* st
   }
 }
 
-template <typename T, int FL>
-__device__ __forceinline__ void epi_rows(const GemmParams& p, EVT_LDS char* stg, int m0, int n,
-                                         int row_lo, int lane, int slot, bool interior) {
-  if (interior) epi_rows_t<T, FL, true>(p, stg, m0, n, row_lo, lane, slot);
-  else epi_rows_t<T, FL, false>(p, stg, m0, n, row_lo, lane, slot);
+// bf16-output form of epi_rows: every lane owns 8 consecutive columns (two staged chunks) of one
+// row, 4 rows per iteration, so each output store is 16 B per lane (dwordx4). Measured: the
+// 8-B-store epilogue is store-issue bound (writing fp32 with 16-B stores was faster than bf16
+// with 8-B stores). Per-row coefficients come from lane (4i + q) via ds_bpermute; statistics
+// partials (16 per row) are parked in the row just consumed and summed in a fixed order.
+// Requires p.vec_ok >= 2 (ldc, ldr, ldp multiples of 8); n = first of the lane's 8 columns.
+template <int FL, bool INTERIOR>
+__device__ __forceinline__ void epi_rows8_t(const GemmParams& p, EVT_LDS char* stg, int m0, int n,
+                                            int row_lo, int lane, int slot) {
+  constexpr bool interior = INTERIOR;
+  const int q = lane >> 4, c8 = lane & 15;
+  const bool col_ok = interior || n < p.N;
+  const bool full = interior || n + 8 <= p.N;
+  f32x4 bias4[2], cs4[2], g4[2], b4[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    bias4[h] = cs4[h] = g4[h] = b4[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool fh = interior || n + 4 * h + 4 <= p.N;
+    if (col_ok) {
+      if (FL & EPI_BIAS) bias4[h] = col4(p.bias, n + 4 * h, p.N, fh);
+      if (FL & EPI_LNIN) cs4[h] = col4(p.colsum, n + 4 * h, p.N, fh);
+      if (FL & EPI_RESLN) {
+        g4[h] = col4(p.rgamma, n + 4 * h, p.N, fh);
+        b4[h] = col4(p.rbeta, n + 4 * h, p.N, fh);
+      }
+    }
+  }
+  float in_mu = 0.f, in_r = 0.f, rs_mu = 0.f, rs_r = 0.f;  // lane c: row row_lo + (c & 31)
+  if (FL & (EPI_LNIN | EPI_RESLN)) {
+    const int mr = m0 + row_lo + (lane & 31);
+    if (interior || mr < p.M) {
+      if (FL & EPI_LNIN) ln_coef(p.stats_in, p.nslots, mr, p.inv_d, p.eps, in_mu, in_r);
+      if (FL & EPI_RESLN) ln_coef(p.rstats, p.nslots, mr, p.inv_d, p.eps, rs_mu, rs_r);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    // bound how many iterations' loads the scheduler hoists (VGPR pressure: the other half of
+    // the accumulators is still live in pass 0)
+    if ((FL & EPI_RESID) ? (i & 1) == 0 && i > 0 : i == 4) __builtin_amdgcn_sched_barrier(0);
+    const int row = row_lo + 4 * i + q;
+    const int m = m0 + row;
+    const bool ok = col_ok && (interior || m < p.M);
+    const int src = (4 * i + q) * 4;  // ds_bpermute byte index of the lane holding this row
+    f32x4 v[2];
+    v[0] = *(const EVT_LDS f32x4*)(stg + stg_off(row, 2 * c8));
+    v[1] = *(const EVT_LDS f32x4*)(stg + stg_off(row, 2 * c8 + 1));
+    int64_t orow = m;
+    if (FL & EPI_LNIN) {
+      const float mu = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, in_mu)));
+      const float r = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, in_r)));
+#pragma unroll
+      for (int h = 0; h < 2; ++h) v[h] = v[h] * r - cs4[h] * (r * mu) + bias4[h];
+    } else if (FL & EPI_BIAS) {
+      v[0] += bias4[0];
+      v[1] += bias4[1];
+    }
+    if (FL & EPI_GELU) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[h][j] = gelu_tanh(v[h][j]);
+    }
+    if (FL & EPI_POS) {
+      const int img = m / p.P, t = m - img * p.P;
+      orow = (int64_t)img * (p.P + 1) + 1 + t;
+      if (ok) {
+        const float* pr = p.pos + (int64_t)(t + 1) * p.ldp;
+        v[0] += col4(pr, n, p.N, interior || n + 4 <= p.N);
+        v[1] += col4(pr, n + 4, p.N, full);
+      }
+    }
+    if (FL & EPI_RESID) {
+      f32x4 rv[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      if (ok) {
+        const bf16* rp = (const bf16*)p.resid + (int64_t)m * p.ldr + n;
+        if (full) {
+          const bf16x8 r8 = __builtin_bit_cast(bf16x8, *(const u32x4*)rp);
+          rv[0] = f32x4{(float)r8[0], (float)r8[1], (float)r8[2], (float)r8[3]};
+          rv[1] = f32x4{(float)r8[4], (float)r8[5], (float)r8[6], (float)r8[7]};
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (n + j < p.N) rv[j >> 2][j & 3] = to_f32(rp[j]);
+        }
+      }
+      if (FL & EPI_RESLN) {
+        const float mu = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, rs_mu)));
+        const float r = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, rs_r)));
+#pragma unroll
+        for (int h = 0; h < 2; ++h) rv[h] = (rv[h] - mu) * r * g4[h] + b4[h];
+      }
+      v[0] += rv[0];
+      v[1] += rv[1];
+    }
+    const bf16x8 o = {(bf16)v[0][0], (bf16)v[0][1], (bf16)v[0][2], (bf16)v[0][3],
+                      (bf16)v[1][0], (bf16)v[1][1], (bf16)v[1][2], (bf16)v[1][3]};
+    if (ok) {
+      bf16* cp = (bf16*)p.C + orow * p.ldc + n;
+      if (full) *(u32x4*)cp = __builtin_bit_cast(u32x4, o);
+      else
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (n + j < p.N) cp[j] = o[j];
+    }
+    if (FL & EPI_STATS) {
+      float s1 = 0.f, s2 = 0.f;
+      if (ok) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = (full || n + j < p.N) ? (float)o[j] : 0.f;
+          s1 += x;
+          s2 += x * x;
+        }
+      }
+      // park in row `row` (read above by these same lanes): partial c8 at byte c8 * 8
+      *(EVT_LDS f32x2*)(stg + row * 512 + c8 * 8) = f32x2{s1, s2};
+    }
+  }
+  if (FL & EPI_STATS) {
+    // lane (r = lane & 31, hf = lane >> 5): row row_lo + r, partials [8 hf, 8 hf + 8)
+    const int r = lane & 31, hf = lane >> 5;
+    const EVT_LDS char* src = stg + (row_lo + r) * 512 + hf * 64;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 v = *(const EVT_LDS f32x4*)(src + j * 16);
+      s1 += v[0] + v[2];
+      s2 += v[1] + v[3];
+    }
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    const int m = m0 + row_lo + r;
+    if (hf == 0 && (interior || m < p.M)) {
+      int64_t orow = m;
+      if (FL & EPI_POS) {
+        const int img = m / p.P, t = m - img * p.P;
+        orow = (int64_t)img * (p.P + 1) + 1 + t;
+      }
+      *(f32x2*)(p.stats_out + 2 * (p.nslots * orow + slot)) = f32x2{s1, s2};
+    }
+  }
+}
+
+// n4: first column of the lane in the 4-column layout (lane chunk c = lane & 31);
+// n8: first column in the 8-column layout (lane chunks 2 (lane & 15), +1).
+// ONLY8: the caller guarantees p.vec_ok >= 2 (the 256x256 kernel), so only the 8-column form is
+// compiled in (the dead 4-column form otherwise costs registers: hoisted addresses spill).
+template <typename T, int FL, bool ONLY8 = false>
+__device__ __forceinline__ void epi_rows(const GemmParams& p, EVT_LDS char* stg, int m0, int n4,
+                                         int n8, int row_lo, int lane, int slot, bool interior) {
+  constexpr bool out16 = std::is_same<T, bf16>::value && !(FL & EPI_OUT_F32);
+  if (out16 && (ONLY8 || p.vec_ok >= 2)) {
+    if (interior) epi_rows8_t<FL, true>(p, stg, m0, n8, row_lo, lane, slot);
+    else epi_rows8_t<FL, false>(p, stg, m0, n8, row_lo, lane, slot);
+    return;
+  }
+  if constexpr (!(out16 && ONLY8)) {
+    if (interior) epi_rows_t<T, FL, true>(p, stg, m0, n4, row_lo, lane, slot);
+    else epi_rows_t<T, FL, false>(p, stg, m0, n4, row_lo, lane, slot);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -312,7 +468,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmParams p) {
     }
   __syncthreads();
   const bool interior = p.vec_ok && (n0 + GEMM_BN <= p.N) && (m0 + GEMM_BM <= p.M);
-  epi_rows<T, FL>(p, stg, m0, n0 + (lane & 31) * 4, wave * 32, lane, n0 / 128, interior);
+  epi_rows<T, FL>(p, stg, m0, n0 + (lane & 31) * 4, n0 + (lane & 15) * 8, wave * 32, lane,
+                  n0 / 128, interior);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -328,14 +485,48 @@ constexpr int BIG_BM = 256, BIG_BN = 256;
 constexpr int BIG_TILE = BIG_BM * ROWB;       // 32 KiB per operand
 constexpr int BIG_STAGE = 2 * BIG_TILE;       // 64 KiB per K-tile
 
-int g_gemm_variant = 0;  // 0 auto, 1 force 128x128, 2 256x256 VAR 0, 6 256x256 VAR 6
+int g_gemm_variant = 0;  // 0 auto, 1 force 128x128, 2 / 6 256x256 VAR 0 / 6
 
-bool use_big(const GemmParams& p) {
+bool use_big(const GemmParams& p, int flags) {
   if ((p.ntiles * GEMM_BN) % BIG_BN) return false;
+  if (!(flags & EPI_OUT_F32) && p.vec_ok < 2) return false;  // big epilogue: 16-B bf16 stores only
   if (g_gemm_variant == 1) return false;
   if (g_gemm_variant >= 2) return true;
   // enough 256x256 tiles to fill the chip at least once
   return (int64_t)((p.M + 255) / 256) * (p.ntiles * GEMM_BN / 256) >= 256;
+}
+
+// Epilogue of the 256x256 kernels: two passes staged through the (idle) 128 KiB of LDS; in
+// pass h every wave hands over its column tiles nt = 2h, 2h+1 (half of its accumulators die per
+// pass) and all 8 waves then stream 32 rows each of the staged 256 x 128 slab. Stats slot of
+// pass h: 2*tn + h. The wave's 128 x 64 sub-tile is rows wm*128.., columns wn*64...
+template <int FL>
+__device__ __forceinline__ void big_epilogue(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
+                                             int wm, int wn, int m0, int n0, int tn, int wave,
+                                             int lane) {
+  EVT_LDS char* stg = (EVT_LDS char*)smem;
+  const bool interior = p.vec_ok && (n0 + BIG_BN <= p.N) && (m0 + BIG_BM <= p.M);
+  const int c = lane & 31, frow = lane & 15, fg = lane >> 4;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    __builtin_amdgcn_s_barrier();  // previous readers of the staging area are done
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) {
+        const int row = wm * 128 + mt * 16 + frow;
+        *(EVT_LDS f32x4*)(stg + stg_off(row, wn * 8 + t * 4 + fg)) = acc[2 * h + t][mt];
+      }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    // staged chunk c holds global columns n0 + (c>>3)*64 + h*32 + (c&7)*4 .. +3
+    // (8-column layout: lane chunks 2 c8, 2 c8 + 1 -> n0 + (c8>>2)*64 + h*32 + (c8&3)*8 .. +7)
+    const int c8 = lane & 15;
+    epi_rows<bf16, FL, true>(p, stg, m0, n0 + (c >> 3) * 64 + h * 32 + (c & 7) * 4,
+                       n0 + (c8 >> 2) * 64 + h * 32 + (c8 & 3) * 8, wave * 32, lane, 2 * tn + h,
+                       interior);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
 }
 
 template <int FL, int VAR>
@@ -436,29 +627,7 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(GemmParams p) {
     }
   }
 
-  // ---- epilogue: two passes staged through the (idle) 128 KiB of LDS; in pass h every wave
-  // hands over its column tiles nt = 2h, 2h+1 (half of its accumulators die per pass) and all 8
-  // waves then stream 32 rows each of the staged 256 x 128 slab. Stats slot of pass h: 2*tn + h.
-  EVT_LDS char* stg = (EVT_LDS char*)smem;
-  const bool interior = p.vec_ok && (n0 + BIG_BN <= p.N) && (m0 + BIG_BM <= p.M);
-  const int c = lane & 31;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    __builtin_amdgcn_s_barrier();  // previous readers of the staging area are done
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int mt = 0; mt < 8; ++mt) {
-        const int row = wm * 128 + mt * 16 + frow;
-        *(EVT_LDS f32x4*)(stg + stg_off(row, wn * 8 + t * 4 + fg)) = acc[2 * h + t][mt];
-      }
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-    // staged chunk c holds global columns n0 + (c>>3)*64 + h*32 + (c&7)*4 .. +3
-    epi_rows<bf16, FL>(p, stg, m0, n0 + (c >> 3) * 64 + h * 32 + (c & 7) * 4, wave * 32, lane,
-                       2 * tn + h, interior);
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-  }
+  big_epilogue<FL>(p, smem, acc, wm, wn, m0, n0, tn, wave, lane);
 }
 
 template <int FL>
@@ -477,7 +646,7 @@ hipError_t launch_big(const GemmParams& p, hipStream_t s) {
 template <typename T, int FL>
 hipError_t launch_t(const GemmParams& p, hipStream_t s) {
   if constexpr (std::is_same<T, bf16>::value) {
-    if (use_big(p)) return launch_big<FL>(p, s);
+    if (use_big(p, FL)) return launch_big<FL>(p, s);
   }
   const int mtiles = (p.M + GEMM_BM - 1) / GEMM_BM;
   hipLaunchKernelGGL((gemm_nt_kernel<T, FL>), dim3(mtiles * p.ntiles), dim3(256), 0, s, p);

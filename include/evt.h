@@ -95,7 +95,8 @@ int evt_model_destroy(evt_model* model);
 
 /* GEMM tile-shape policy for bf16 (process-wide tuning knob): 0 = automatic (256x256 tiles when
  * the problem has >= 256 of them, else 128x128), 1 = always 128x128, 2 / 6 = 256x256 tiles with
- * the plain / interleaved main loop whenever the packed width allows. */
+ * the plain / interleaved main loop whenever the packed width allows (and the output rows are
+ * 16-B aligned for bf16). */
 int evt_set_gemm_variant(int variant);
 
 /* Pack a Keras [K, N] fp32 kernel into the GEMM operand layout Wp[Npad][Kpad] (dtype), zero

@@ -18,7 +18,15 @@ VARS = [int(v) for v in sys.argv[2].split(',')] if len(sys.argv) > 2 else [1, 2,
 shapes = {"qkv": (768, 2304, 0), "out": (768, 768, 21), "fc1": (768, 3072, 3), "fc2": (3072, 768, 21),
           "nt3072": (3072, 768, 0), "nt768x3072": (768, 3072, 0)}
 import os
-shapes = {k: v for k, v in shapes.items() if k in os.environ.get("GS", "qkv,out,fc1,fc2").split(",")}
+sel = os.environ.get("GS", "qkv,out,fc1,fc2").split(",")
+# custom shapes: "KxN" or "KxN@flags" (e.g. 4096x4096@0)
+for it in sel:
+    if "x" in it and it not in shapes:
+        kn, _, fl = it.partition("@")
+        k, n = kn.split("x")
+        shapes[it] = (int(k), int(n), int(fl or 0))
+shapes = {k: v for k, v in shapes.items() if k in sel}
+LDC_PAD = int(os.environ.get("LDC_PAD", "0"))  # extra output row pitch (elements)
 res = {}
 g = torch.Generator(device="cuda").manual_seed(0)
 for name, (K, N, fl) in shapes.items():
@@ -31,12 +39,13 @@ for name, (K, N, fl) in shapes.items():
     R = torch.randn((M, N), generator=g, device="cuda").bfloat16()
     outs = {}
     for v in VARS:
-        outs[v] = torch.empty((M, N), dtype=torch.float32 if fl & 16 else torch.bfloat16, device="cuda")
+        outs[v] = torch.empty((M, N + LDC_PAD), dtype=torch.float32 if fl & 16 else torch.bfloat16,
+                              device="cuda")
     def run(v):
         lib.evt_set_gemm_variant(v)
         a = _lib.evt_dense_args()
         a.flags, a.A, a.lda, a.Wp, a.Kpad, a.Npad = fl, A.data_ptr(), K, wp.data_ptr(), K, npad
-        a.C, a.ldc, a.M, a.N, a.bias = outs[v].data_ptr(), N, M, N, bias.data_ptr()
+        a.C, a.ldc, a.M, a.N, a.bias = outs[v].data_ptr(), N + LDC_PAD, M, N, bias.data_ptr()
         if fl & 4:
             a.resid, a.ldr = R.data_ptr(), N
         _lib.check(lib.evt_dense(1, ctypes.byref(a), S()))
@@ -44,7 +53,7 @@ for name, (K, N, fl) in shapes.items():
     for v in VARS:
         run(v)
     torch.cuda.synchronize()
-    diff = max((outs[VARS[0]].float() - outs[v].float()).abs().max().item() for v in VARS)
+    diff = max((outs[VARS[0]][:, :N].float() - outs[v][:, :N].float()).abs().max().item() for v in VARS)
     for rnd in range(5):
         for v in VARS:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -54,8 +63,23 @@ for name, (K, N, fl) in shapes.items():
             e1.record()
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1) / 10)
+    if os.environ.get("TORCHMM") == "1":  # vendor GEMM (hipBLASLt via torch) on the same operands
+        Wt = W.bfloat16().contiguous()
+        Ct = torch.empty((M, N), dtype=torch.bfloat16, device="cuda")
+        for _ in range(3):
+            torch.matmul(A, Wt, out=Ct)
+        tt = []
+        for rnd in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                torch.matmul(A, Wt, out=Ct)
+            e1.record()
+            torch.cuda.synchronize()
+            tt.append(e0.elapsed_time(e1) / 10)
+        times["torch"] = tt
     fl_ = 2.0 * M * N * K
-    res[name] = {f"v{v}": {"ms": round(sorted(t)[2], 4), "tflops": round(fl_ / (sorted(t)[2] / 1e3) / 1e12, 1)}
+    res[name] = {(f"v{v}" if v != "torch" else v): {"ms": round(sorted(t)[2], 4), "tflops": round(fl_ / (sorted(t)[2] / 1e3) / 1e12, 1)}
                  for v, t in times.items()}
     res[name]["maxdiff_vs_v1"] = diff
     print(name, json.dumps(res[name]), flush=True)

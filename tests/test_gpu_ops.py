@@ -32,7 +32,8 @@ def _gelu(x):
 
 @pytest.mark.parametrize("dtype", ["bf16", "f32"])
 @pytest.mark.parametrize("M,K,N", [(197, 192, 576), (394, 768, 2304), (131, 320, 37 * 4),
-                                   (1000, 576, 192), (64, 64, 1000), (257, 3072, 768)])
+                                   (1000, 576, 192), (64, 64, 1000), (257, 3072, 768),
+                                   (300, 128, 200)])
 @pytest.mark.parametrize("flags", [0, 3, 21, 17])
 @pytest.mark.parametrize("variant", [1, 2, 0])
 def test_dense(gpu, dtype, M, K, N, flags, variant):
