@@ -53,7 +53,16 @@ class evt_dense_args(ctypes.Structure):
                 ("P", ctypes.c_int32), ("colsum", ctypes.c_void_p), ("stats_in", ctypes.c_void_p),
                 ("rstats", ctypes.c_void_p), ("rgamma", ctypes.c_void_p),
                 ("rbeta", ctypes.c_void_p), ("stats_out", ctypes.c_void_p),
-                ("ln_width", ctypes.c_int32), ("ln_eps", ctypes.c_float)]
+                ("ln_width", ctypes.c_int32), ("ln_eps", ctypes.c_float),
+                ("stats_step", ctypes.c_int32)]
+
+
+class evt_t2t_desc(ctypes.Structure):
+    _fields_ = [("image_size", ctypes.c_int32), ("in_chans", ctypes.c_int32),
+                ("num_classes", ctypes.c_int32), ("dim", ctypes.c_int32),
+                ("depth", ctypes.c_int32), ("heads", ctypes.c_int32),
+                ("mlp_dim", ctypes.c_int32), ("token_size", ctypes.c_int32),
+                ("dtype", ctypes.c_int32), ("max_batch", ctypes.c_int32)]
 
 
 # name -> (restype, argtypes); this is the full symbol list of include/evt.h
@@ -74,6 +83,16 @@ SIGNATURES = {
     "evt_attention": (_I, [_I, _P, _I64, _P, _I64, _I, _I, _I, _F, _P]),
     "evt_layernorm": (_I, [_I, _P, _I64, _P, _I64, _P, _P, _I, _I, _F, _P]),
     "evt_patchify": (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P]),
+    "evt_t2t_num_weights": (_I, [ctypes.POINTER(evt_t2t_desc)]),
+    "evt_t2t_create": (_I, [ctypes.POINTER(evt_t2t_desc), ctypes.POINTER(_P), _I, _P,
+                            ctypes.POINTER(_P)]),
+    "evt_t2t_forward": (_I, [_P, _P, _I, _P, _P]),
+    "evt_t2t_query_workspace": (_I, [ctypes.POINTER(evt_t2t_desc), _I,
+                                     ctypes.POINTER(ctypes.c_size_t)]),
+    "evt_unfold": (_I, [_I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P]),
+    "evt_performer": (_I, [_I, _P, _I64, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                           _I64, _P]),
+    "evt_performer_scratch": (_I64, [_I, _I]),
 }
 
 _lib = None

@@ -75,14 +75,32 @@ struct Shape {
 
 }  // namespace
 
+struct Performer {  // one TokenPerformer (transformer_encoder.py:39-101)
+  int din = 0, dpad = 0;     // unfolded input width, padded to PAD_K
+  DenseW kqv;                // LN1-folded Dense(3*64) + bias
+  PerformerWeights w{};      // fp32 device copies (Keras layouts)
+};
+
 struct evt_model {
-  evt_vit_desc desc{};
+  int family = 0;            // 0: ViT / ViT_Pruned, 1: T2T-ViT
+  int dtype = 0, D = 0, max_batch = 0, num_classes = 0;
+  evt_vit_desc desc{};       // ViT only
+  evt_t2t_desc tdesc{};      // T2T only
   std::vector<int32_t> heads, head_dim, ffn;
   Shape sh;
   DenseW patch, head1, head2;
   float *cls = nullptr, *pos = nullptr;
   std::vector<Layer> layers;
   std::vector<void*> allocs;
+  // T2T stage
+  Performer perf[2];
+  DenseW project, head;      // head: LN-folded classifier (final LayerNorm, t2t_vit.py:129,134)
+  int grid[3] = {0, 0, 0};   // token grids S/4, S/8, S/16
+  void* u = nullptr;         // unfold output (GEMM A operand)
+  float* su = nullptr;       // unfold row statistics
+  void* kqvb = nullptr;      // [B*T1, 192]
+  void* pout = nullptr;      // [B*T1, 64] performer output (NHWC for the next unfold)
+  float* part = nullptr;     // performer partial sums
   // workspace (activation dtype unless noted)
   void* apatch = nullptr;    // [B*P, pd] patch matrix (aliases hbuf)
   void* x = nullptr;         // [B*T, D] token stream at layer input / output
@@ -149,7 +167,7 @@ int validate(const evt_vit_desc* d, Shape* sh) {
 // weights alongside (gemm.hip, "LayerNorm folding").
 int make_dense(evt_model* m, DenseW* dw, const float* W, const float* bias, int K, int N,
                hipStream_t s, const float* ln_g = nullptr, const float* ln_b = nullptr) {
-  const int dt = m->desc.dtype;
+  const int dt = m->dtype;
   dw->K = K;
   dw->N = N;
   dw->kpad = (int)round_up(K, PAD_K);
@@ -202,6 +220,8 @@ struct DenseCall {
   const float* rgamma = nullptr;
   const float* rbeta = nullptr;
   float* stats_out = nullptr;
+  int ln_width = 0;    // LayerNorm width of stats_in / rstats / stats_out (0: the model width D)
+  int stats_step = 1;  // EPI_LNIN: A row m reads stats_in row m * stats_step
 };
 
 int dense(const evt_model* m, const DenseW& w, const DenseCall& c, hipStream_t s) {
@@ -232,11 +252,165 @@ int dense(const evt_model* m, const DenseW& w, const DenseCall& c, hipStream_t s
   p.rgamma = c.rgamma;
   p.rbeta = c.rbeta;
   p.stats_out = c.stats_out;
-  p.inv_d = 1.0f / (float)m->desc.dim;
+  const int width = c.ln_width ? c.ln_width : m->D;
+  p.inv_d = 1.0f / (float)width;
   p.eps = 1e-5f;  // Keras LayerNormalization(epsilon=1e-5), reference norm.py:6
-  p.nslots = stats_slots(m->desc.dim);
-  EVT_HIP(gemm_launch(m->desc.dtype, c.flags, p, s), "dense");
+  p.nslots = stats_slots(width);
+  p.stats_step = c.stats_step;
+  EVT_HIP(gemm_launch(m->dtype, c.flags, p, s), "dense");
   return EVT_OK;
+}
+
+
+// Encoder weights (11 tensors per layer, evt_vit_num_weights order) for m->heads / m->ffn.
+int build_encoder(evt_model* m, const float* const* w, hipStream_t s) {
+  const int D = m->D;
+  const int depth = (int)m->heads.size();
+  m->layers.resize(depth);
+  int k = 0;
+  for (int i = 0; i < depth; ++i) {
+    Layer& L = m->layers[i];
+    L.heads = m->heads[i];
+    L.inner = L.heads * 64;
+    L.ffn = m->ffn[i];
+    L.ffn_st = (int)round_up(L.ffn, PAD_N);
+    EVT_RC(copy_vec(m, &L.ln1_g, w[k + 0], D, s));
+    EVT_RC(copy_vec(m, &L.ln1_b, w[k + 1], D, s));
+    EVT_RC(make_dense(m, &L.qkv, w[k + 2], nullptr, D, 3 * L.inner, s, w[k + 0], w[k + 1]));
+    EVT_RC(make_dense(m, &L.out, w[k + 3], w[k + 4], L.inner, D, s));
+    EVT_RC(copy_vec(m, &L.ln2_g, w[k + 5], D, s));
+    EVT_RC(copy_vec(m, &L.ln2_b, w[k + 6], D, s));
+    EVT_RC(make_dense(m, &L.fc1, w[k + 7], w[k + 8], D, L.ffn, s, w[k + 5], w[k + 6]));
+    EVT_RC(make_dense(m, &L.fc2, w[k + 9], w[k + 10], L.ffn, D, s));
+    k += 11;
+  }
+  return EVT_OK;
+}
+
+// Token-stream workspace of the encoder for B images (hbuf_bytes: the FFN hidden buffer).
+int alloc_encoder_ws(evt_model* m, int B, size_t hbuf_bytes) {
+  const size_t es = elem_size(m->dtype);
+  const size_t rows = (size_t)B * m->sh.T;
+  EVT_RC(dev_alloc(m, &m->x, rows * m->D * es));
+  EVT_RC(dev_alloc(m, &m->xm, rows * m->D * es));
+  const size_t stats_bytes = rows * stats_slots(m->D) * 2 * sizeof(float);
+  EVT_RC(dev_alloc(m, (void**)&m->sx, stats_bytes));
+  EVT_RC(dev_alloc(m, (void**)&m->sm, stats_bytes));
+  EVT_RC(dev_alloc(m, &m->qkv, rows * 3 * m->sh.max_inner * es));
+  EVT_RC(dev_alloc(m, &m->o, rows * m->sh.max_inner * es));
+  EVT_RC(dev_alloc(m, &m->hbuf, hbuf_bytes));
+  return EVT_OK;
+}
+
+// Encoder layers (transformer_encoder.py:13-18 / :26-34) on the token stream m->x (+ stats sx).
+int run_encoder(evt_model* m, int B, hipStream_t s) {
+  const int D = m->D, T = m->sh.T, rows = B * T;
+  const float log2e = 1.4426950408889634f;
+  for (const Layer& L : m->layers) {
+    {  // LN1-folded QKV (attention.py:24)
+      DenseCall c;
+      c.flags = EPI_LNIN | EPI_BIAS;
+      c.A = m->x; c.lda = D; c.C = m->qkv; c.ldc = 3 * L.inner; c.M = rows; c.N = 3 * L.inner;
+      c.stats_in = m->sx;
+      EVT_RC(dense(m, L.qkv, c, s));
+    }
+    AttnParams ap{m->qkv, 3 * L.inner, m->o, L.inner, T, L.heads, B, 0.125f * log2e};
+    EVT_HIP(attention_launch(m->dtype, ap, s), "attention");
+    {  // out-proj + bias + LN1(x) residual -> xm (+ stats)
+      DenseCall c;
+      c.flags = EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS;
+      c.A = m->o; c.lda = L.inner; c.C = m->xm; c.ldc = D; c.M = rows; c.N = D;
+      c.resid = m->x; c.ldr = D; c.rstats = m->sx; c.rgamma = L.ln1_g; c.rbeta = L.ln1_b;
+      c.stats_out = m->sm;
+      EVT_RC(dense(m, L.out, c, s));
+    }
+    {  // LN2-folded FC1 + GELU (ffn.py:8)
+      DenseCall c;
+      c.flags = EPI_LNIN | EPI_BIAS | EPI_GELU;
+      c.A = m->xm; c.lda = D; c.C = m->hbuf; c.ldc = L.ffn_st; c.M = rows; c.N = L.ffn_st;
+      c.stats_in = m->sm;
+      EVT_RC(dense(m, L.fc1, c, s));
+    }
+    {  // FC2 + bias + LN2(xm) residual -> x (+ stats)
+      DenseCall c;
+      c.flags = EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS;
+      c.A = m->hbuf; c.lda = L.ffn_st; c.C = m->x; c.ldc = D; c.M = rows; c.N = D;
+      c.resid = m->xm; c.ldr = D; c.rstats = m->sm; c.rgamma = L.ln2_g; c.rbeta = L.ln2_b;
+      c.stats_out = m->sx;
+      EVT_RC(dense(m, L.fc2, c, s));
+    }
+  }
+  return EVT_OK;
+}
+
+int finish_create(evt_model* m, int rc, evt_model** out) {
+  if (rc) {
+    std::string keep = g_err;
+    evt_model_destroy(m);
+    g_err = keep;
+    return rc;
+  }
+  *out = m;
+  return EVT_OK;
+}
+
+struct T2TShape {
+  Shape enc;             // encoder geometry (P = (S/16)^2 patches, T = P + 1)
+  int grid[3] = {0, 0, 0};
+  int din[2] = {0, 0};   // unfolded widths feeding performer 1 / 2
+};
+
+int validate_t2t(const evt_t2t_desc* d, T2TShape* ts) {
+  if (!d) return fail(EVT_EINVAL, "desc is NULL");
+  if (d->dtype != EVT_DTYPE_F32 && d->dtype != EVT_DTYPE_BF16)
+    return fail(EVT_EINVAL, "dtype must be EVT_DTYPE_F32 or EVT_DTYPE_BF16");
+  if (d->image_size <= 0 || d->image_size % 16)
+    return fail(EVT_EINVAL, "image_size must be a positive multiple of 16");
+  if (d->in_chans <= 0 || d->num_classes <= 0 || d->depth < 0 || d->mlp_dim <= 0)
+    return fail(EVT_EINVAL, "in_chans, num_classes, mlp_dim must be positive, depth >= 0");
+  if (d->dim <= 0 || d->dim % 64 != 0 || d->dim > 1024)
+    return fail(EVT_EINVAL, "dim must be a positive multiple of 64 and <= 1024");
+  if (d->heads <= 0 || d->dim % d->heads != 0)  // Attention raises ValueError (attention.py:8-9)
+    return fail(EVT_EINVAL, "hidden_size must be a multiple of num_heads");
+  if (d->dim / d->heads != 64) return fail(EVT_EINVAL, "head size must be 64 in this build");
+  if (d->token_size != 64) return fail(EVT_EINVAL, "token_size must be 64 in this build");
+  if (d->max_batch <= 0) return fail(EVT_EINVAL, "max_batch must be positive");
+  const int S = d->image_size;
+  ts->grid[0] = S / 4;
+  ts->grid[1] = S / 8;
+  ts->grid[2] = S / 16;
+  ts->din[0] = 49 * d->in_chans;
+  ts->din[1] = 9 * 64;
+  Shape& sh = ts->enc;
+  sh.P = ts->grid[2] * ts->grid[2];
+  sh.T = sh.P + 1;
+  if (sh.T > 256) return fail(EVT_EINVAL, "at most 255 patches per image are supported");
+  sh.D = d->dim;
+  sh.pd = 9 * 64;
+  sh.max_inner = d->heads * 64;
+  sh.max_ffn_st = (int)round_up(d->mlp_dim, PAD_N);
+  sh.head_st = 0;
+  return EVT_OK;
+}
+
+size_t t2t_unfold_elems(const T2TShape& ts, int B) {
+  const size_t t1 = (size_t)ts.grid[0] * ts.grid[0], t2 = (size_t)ts.grid[1] * ts.grid[1];
+  const size_t t3 = (size_t)ts.grid[2] * ts.grid[2];
+  return (size_t)B * std::max({t1 * round_up(ts.din[0], PAD_K), t2 * ts.din[1], t3 * ts.din[1]});
+}
+
+size_t t2t_unfold_stat_floats(const T2TShape& ts, int B) {
+  const size_t t1 = (size_t)ts.grid[0] * ts.grid[0], t2 = (size_t)ts.grid[1] * ts.grid[1];
+  return (size_t)B * std::max(t1 * stats_slots(ts.din[0]), t2 * stats_slots(ts.din[1])) * 2;
+}
+
+size_t t2t_workspace_bytes(const evt_t2t_desc* d, const T2TShape& ts, int B) {
+  const size_t es = elem_size(d->dtype);
+  const size_t rows = (size_t)B * ts.enc.T, t1 = (size_t)B * ts.grid[0] * ts.grid[0];
+  return t2t_unfold_elems(ts, B) * es + t2t_unfold_stat_floats(ts, B) * 4 + t1 * 4 * 64 * es +
+         performer_part_floats(B, ts.grid[0] * ts.grid[0]) * 4 + 2 * rows * d->dim * es +
+         2 * rows * stats_slots(d->dim) * 2 * 4 + rows * 4 * ts.enc.max_inner * es +
+         rows * ts.enc.max_ffn_st * es;
 }
 
 }  // namespace
@@ -290,6 +464,11 @@ int evt_vit_create(const evt_vit_desc* desc, const float* const* w, int n_weight
     if (!w[i]) return fail(EVT_EINVAL, "weight pointer " + std::to_string(i) + " is NULL");
   hipStream_t s = (hipStream_t)stream;
   evt_model* m = new evt_model();
+  m->family = 0;
+  m->dtype = desc->dtype;
+  m->D = desc->dim;
+  m->max_batch = desc->max_batch;
+  m->num_classes = desc->num_classes;
   m->desc = *desc;
   m->heads.assign(desc->heads, desc->heads + desc->depth);
   m->head_dim.assign(desc->head_dim, desc->head_dim + desc->depth);
@@ -303,64 +482,32 @@ int evt_vit_create(const evt_vit_desc* desc, const float* const* w, int n_weight
     EVT_RC(make_dense(m, &m->patch, w[0], w[1], sh.pd, D, s));
     EVT_RC(copy_vec(m, &m->cls, w[2], D, s));
     EVT_RC(copy_vec(m, &m->pos, w[3], (size_t)sh.T * D, s));
-    int k = 4;
-    m->layers.resize(desc->depth);
-    for (int i = 0; i < desc->depth; ++i) {
-      Layer& L = m->layers[i];
-      L.heads = desc->heads[i];
-      L.inner = L.heads * 64;
-      L.ffn = desc->ffn[i];
-      L.ffn_st = (int)round_up(L.ffn, PAD_N);
-      EVT_RC(copy_vec(m, &L.ln1_g, w[k + 0], D, s));
-      EVT_RC(copy_vec(m, &L.ln1_b, w[k + 1], D, s));
-      EVT_RC(make_dense(m, &L.qkv, w[k + 2], nullptr, D, 3 * L.inner, s, w[k + 0], w[k + 1]));
-      EVT_RC(make_dense(m, &L.out, w[k + 3], w[k + 4], L.inner, D, s));
-      EVT_RC(copy_vec(m, &L.ln2_g, w[k + 5], D, s));
-      EVT_RC(copy_vec(m, &L.ln2_b, w[k + 6], D, s));
-      EVT_RC(make_dense(m, &L.fc1, w[k + 7], w[k + 8], D, L.ffn, s, w[k + 5], w[k + 6]));
-      EVT_RC(make_dense(m, &L.fc2, w[k + 9], w[k + 10], L.ffn, D, s));
-      k += 11;
-    }
+    EVT_RC(build_encoder(m, w + 4, s));
+    const int k = 4 + 11 * desc->depth;
     EVT_RC(make_dense(m, &m->head1, w[k + 0], w[k + 1], D, desc->mlp_dim, s));
     EVT_RC(make_dense(m, &m->head2, w[k + 2], w[k + 3], desc->mlp_dim, desc->num_classes, s));
-    // workspace
     const int B = desc->max_batch;
     const size_t es = elem_size(desc->dtype);
-    const size_t rows = (size_t)B * sh.T;
-    EVT_RC(dev_alloc(m, &m->x, rows * D * es));
-    EVT_RC(dev_alloc(m, &m->xm, rows * D * es));
-    const size_t stats_bytes = rows * stats_slots(D) * 2 * sizeof(float);
-    EVT_RC(dev_alloc(m, (void**)&m->sx, stats_bytes));
-    EVT_RC(dev_alloc(m, (void**)&m->sm, stats_bytes));
-    EVT_RC(dev_alloc(m, &m->qkv, rows * 3 * sh.max_inner * es));
-    EVT_RC(dev_alloc(m, &m->o, rows * sh.max_inner * es));
-    EVT_RC(dev_alloc(m, &m->hbuf, std::max(rows * sh.max_ffn_st, (size_t)B * sh.P * sh.pd) * es));
+    EVT_RC(alloc_encoder_ws(m, B, std::max((size_t)B * sh.T * sh.max_ffn_st,
+                                           (size_t)B * sh.P * sh.pd) * es));
     m->apatch = m->hbuf;
     EVT_RC(dev_alloc(m, &m->hh, (size_t)B * sh.head_st * es));
     m->ws_bytes = workspace_bytes(desc, sh, B);
     EVT_HIP(hipStreamSynchronize(s), "create sync");
     return EVT_OK;
   };
-  int rc = run();
-  if (rc) {
-    std::string keep = g_err;
-    evt_model_destroy(m);
-    g_err = keep;
-    return rc;
-  }
-  *out = m;
-  return EVT_OK;
+  return finish_create(m, run(), out);
 }
 
 int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* stream) {
   if (!m || !img || !logits) return fail(EVT_EINVAL, "model, img and logits must be non-null");
-  if (B <= 0 || B > m->desc.max_batch)
-    return fail(EVT_EINVAL,
-                "batch must be in [1, max_batch=" + std::to_string(m->desc.max_batch) + "]");
+  if (m->family != 0) return fail(EVT_EINVAL, "model is not a ViT (use evt_t2t_forward)");
+  if (B <= 0 || B > m->max_batch)
+    return fail(EVT_EINVAL, "batch must be in [1, max_batch=" + std::to_string(m->max_batch) + "]");
   hipStream_t s = (hipStream_t)stream;
   const evt_vit_desc& d = m->desc;
   const Shape& sh = m->sh;
-  const int D = d.dim, T = sh.T, rows = B * T, dt = d.dtype;
+  const int D = d.dim, T = sh.T, dt = d.dtype;
   // patch embedding (vit.py:45-51): rearrange -> Dense(D) + pos, CLS row = cls + pos[0]
   EVT_HIP(patchify_launch(dt, img, B, d.in_chans, d.image_size, d.patch_size, m->apatch, m->x,
                           m->cls, m->pos, D, m->sx, s),
@@ -372,41 +519,7 @@ int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* 
     c.pos = m->pos; c.ldp = D; c.P = sh.P; c.stats_out = m->sx;
     EVT_RC(dense(m, m->patch, c, s));
   }
-  const float log2e = 1.4426950408889634f;
-  for (const Layer& L : m->layers) {
-    {  // LN1-folded QKV (attention.py:24)
-      DenseCall c;
-      c.flags = EPI_LNIN | EPI_BIAS;
-      c.A = m->x; c.lda = D; c.C = m->qkv; c.ldc = 3 * L.inner; c.M = rows; c.N = 3 * L.inner;
-      c.stats_in = m->sx;
-      EVT_RC(dense(m, L.qkv, c, s));
-    }
-    AttnParams ap{m->qkv, 3 * L.inner, m->o, L.inner, T, L.heads, B, 0.125f * log2e};
-    EVT_HIP(attention_launch(dt, ap, s), "attention");
-    {  // out-proj + bias + LN1(x) residual -> xm (+ stats)
-      DenseCall c;
-      c.flags = EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS;
-      c.A = m->o; c.lda = L.inner; c.C = m->xm; c.ldc = D; c.M = rows; c.N = D;
-      c.resid = m->x; c.ldr = D; c.rstats = m->sx; c.rgamma = L.ln1_g; c.rbeta = L.ln1_b;
-      c.stats_out = m->sm;
-      EVT_RC(dense(m, L.out, c, s));
-    }
-    {  // LN2-folded FC1 + GELU (ffn.py:8)
-      DenseCall c;
-      c.flags = EPI_LNIN | EPI_BIAS | EPI_GELU;
-      c.A = m->xm; c.lda = D; c.C = m->hbuf; c.ldc = L.ffn_st; c.M = rows; c.N = L.ffn_st;
-      c.stats_in = m->sm;
-      EVT_RC(dense(m, L.fc1, c, s));
-    }
-    {  // FC2 + bias + LN2(xm) residual -> x (+ stats)
-      DenseCall c;
-      c.flags = EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS;
-      c.A = m->hbuf; c.lda = L.ffn_st; c.C = m->x; c.ldc = D; c.M = rows; c.N = D;
-      c.resid = m->xm; c.ldr = D; c.rstats = m->sm; c.rgamma = L.ln2_g; c.rbeta = L.ln2_b;
-      c.stats_out = m->sx;
-      EVT_RC(dense(m, L.fc2, c, s));
-    }
-  }
+  EVT_RC(run_encoder(m, B, s));
   // head on token 0 (vit.py:54-55; no final LayerNorm): rows b*T of the stream, stride T*D
   {
     DenseCall c;
@@ -420,6 +533,145 @@ int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* 
     c.A = m->hh; c.lda = sh.head_st; c.C = logits; c.ldc = d.num_classes; c.M = B;
     c.N = d.num_classes;
     EVT_RC(dense(m, m->head2, c, s));
+  }
+  return EVT_OK;
+}
+
+// ---- T2T-ViT ----------------------------------------------------------------------------
+
+int evt_t2t_num_weights(const evt_t2t_desc* desc) {
+  if (!desc || desc->depth < 0) return fail(EVT_EINVAL, "bad desc");
+  return 2 * 13 + 4 + 11 * desc->depth + 4;
+}
+
+int evt_t2t_query_workspace(const evt_t2t_desc* desc, int batch, size_t* bytes) {
+  T2TShape ts;
+  EVT_RC(validate_t2t(desc, &ts));
+  if (!bytes || batch <= 0) return fail(EVT_EINVAL, "bytes must be non-null and batch positive");
+  *bytes = t2t_workspace_bytes(desc, ts, batch);
+  return EVT_OK;
+}
+
+int evt_t2t_create(const evt_t2t_desc* desc, const float* const* w, int n_weights, void* stream,
+                   evt_model** out) {
+  if (!out) return fail(EVT_EINVAL, "out is NULL");
+  *out = nullptr;
+  T2TShape ts;
+  EVT_RC(validate_t2t(desc, &ts));
+  if (n_weights != evt_t2t_num_weights(desc) || !w)
+    return fail(EVT_EINVAL, "expected " + std::to_string(evt_t2t_num_weights(desc)) + " weights");
+  for (int i = 0; i < n_weights; ++i)
+    if (!w[i]) return fail(EVT_EINVAL, "weight pointer " + std::to_string(i) + " is NULL");
+  hipStream_t s = (hipStream_t)stream;
+  evt_model* m = new evt_model();
+  m->family = 1;
+  m->dtype = desc->dtype;
+  m->D = desc->dim;
+  m->max_batch = desc->max_batch;
+  m->num_classes = desc->num_classes;
+  m->tdesc = *desc;
+  m->heads.assign(desc->depth, desc->heads);
+  m->head_dim.assign(desc->depth, 64);
+  m->ffn.assign(desc->depth, desc->mlp_dim);
+  m->sh = ts.enc;
+  for (int i = 0; i < 3; ++i) m->grid[i] = ts.grid[i];
+  const int D = desc->dim;
+  auto run = [&]() -> int {
+    int k = 0;
+    for (int pi = 0; pi < 2; ++pi) {  // transformer_encoder.py:43-65
+      Performer& P = m->perf[pi];
+      P.din = ts.din[pi];
+      P.dpad = (int)round_up(P.din, PAD_K);
+      EVT_RC(make_dense(m, &P.kqv, w[k + 2], w[k + 3], P.din, 3 * 64, s, w[k + 0], w[k + 1]));
+      const float* src[9] = {w[k + 4], w[k + 5], w[k + 6], w[k + 7], w[k + 8],
+                             w[k + 9], w[k + 10], w[k + 11], w[k + 12]};
+      const size_t len[9] = {32 * 64, 64 * 64, 64, 64, 64, 64 * 64, 64, 64 * 64, 64};
+      float* dst[9];
+      for (int j = 0; j < 9; ++j) EVT_RC(copy_vec(m, &dst[j], src[j], len[j], s));
+      P.w = PerformerWeights{dst[0], dst[1], dst[2], dst[3], dst[4], dst[5], dst[6], dst[7], dst[8]};
+      k += 13;
+    }
+    EVT_RC(make_dense(m, &m->project, w[k + 0], w[k + 1], 9 * 64, D, s));  // t2t_vit.py:56,86
+    EVT_RC(copy_vec(m, &m->cls, w[k + 2], D, s));
+    EVT_RC(copy_vec(m, &m->pos, w[k + 3], (size_t)ts.enc.T * D, s));
+    k += 4;
+    EVT_RC(build_encoder(m, w + k, s));
+    k += 11 * desc->depth;
+    // final LayerNorm (t2t_vit.py:111,129) folded into the classifier (:114,134)
+    EVT_RC(make_dense(m, &m->head, w[k + 2], w[k + 3], D, desc->num_classes, s, w[k + 0], w[k + 1]));
+    const int B = desc->max_batch;
+    const size_t es = elem_size(desc->dtype);
+    const size_t t1 = (size_t)B * ts.grid[0] * ts.grid[0];
+    EVT_RC(dev_alloc(m, &m->u, t2t_unfold_elems(ts, B) * es));
+    EVT_RC(dev_alloc(m, (void**)&m->su, t2t_unfold_stat_floats(ts, B) * sizeof(float)));
+    EVT_RC(dev_alloc(m, &m->kqvb, t1 * 3 * 64 * es));
+    EVT_RC(dev_alloc(m, &m->pout, t1 * 64 * es));
+    EVT_RC(dev_alloc(m, (void**)&m->part, performer_part_floats(B, ts.grid[0] * ts.grid[0]) *
+                                              sizeof(float)));
+    EVT_RC(alloc_encoder_ws(m, B, (size_t)B * ts.enc.T * ts.enc.max_ffn_st * es));
+    m->ws_bytes = t2t_workspace_bytes(desc, ts, B);
+    EVT_HIP(hipStreamSynchronize(s), "create sync");
+    return EVT_OK;
+  };
+  return finish_create(m, run(), out);
+}
+
+int evt_t2t_forward(evt_model* m, const float* img, int B, float* logits, void* stream) {
+  if (!m || !img || !logits) return fail(EVT_EINVAL, "model, img and logits must be non-null");
+  if (m->family != 1) return fail(EVT_EINVAL, "model is not a T2T-ViT (use evt_vit_forward)");
+  if (B <= 0 || B > m->max_batch)
+    return fail(EVT_EINVAL, "batch must be in [1, max_batch=" + std::to_string(m->max_batch) + "]");
+  hipStream_t s = (hipStream_t)stream;
+  const evt_t2t_desc& d = m->tdesc;
+  const int dt = d.dtype, D = d.dim, T = m->sh.T, P = m->sh.P, S = d.image_size;
+  const int g1 = m->grid[0], g2 = m->grid[1];
+  const int t1 = g1 * g1, t2 = g2 * g2;
+  // iteration 1: soft_split0 (k7 s4 p2) of the NHWC image -> TokenPerformer    (t2t_vit.py:66-68)
+  const Performer& P1 = m->perf[0];
+  EVT_HIP(unfold_launch(dt, 1, img, B, S, S, d.in_chans, 7, 4, 2, m->u, P1.dpad, m->su,
+                        stats_slots(P1.din), s),
+          "soft_split0");
+  {
+    DenseCall c;
+    c.flags = EPI_LNIN | EPI_BIAS;
+    c.A = m->u; c.lda = P1.dpad; c.C = m->kqvb; c.ldc = 3 * 64; c.M = B * t1; c.N = 3 * 64;
+    c.stats_in = m->su; c.ln_width = P1.din;
+    EVT_RC(dense(m, P1.kqv, c, s));
+  }
+  EVT_HIP(performer_launch(dt, m->kqvb, 3 * 64, B, t1, P1.w, m->part, m->pout, 64, s),
+          "performer1");
+  // iteration 2: soft_split1 (k3 s2 p1) of the [B, S/4, S/4, 64] map -> TokenPerformer (:72-77)
+  const Performer& P2 = m->perf[1];
+  EVT_HIP(unfold_launch(dt, 0, m->pout, B, g1, g1, 64, 3, 2, 1, m->u, P2.dpad, m->su,
+                        stats_slots(P2.din), s),
+          "soft_split1");
+  {
+    DenseCall c;
+    c.flags = EPI_LNIN | EPI_BIAS;
+    c.A = m->u; c.lda = P2.dpad; c.C = m->kqvb; c.ldc = 3 * 64; c.M = B * t2; c.N = 3 * 64;
+    c.stats_in = m->su; c.ln_width = P2.din;
+    EVT_RC(dense(m, P2.kqv, c, s));
+  }
+  EVT_HIP(performer_launch(dt, m->kqvb, 3 * 64, B, t2, P2.w, m->part, m->pout, 64, s),
+          "performer2");
+  // soft_split2 -> project Dense(D) into token rows 1..P, + CLS row, + sinusoid pos (:81-86,121-125)
+  EVT_HIP(unfold_launch(dt, 0, m->pout, B, g2, g2, 64, 3, 2, 1, m->u, 9 * 64, nullptr, 0, s),
+          "soft_split2");
+  EVT_HIP(cls_rows_launch(dt, m->x, B, T, D, m->cls, m->pos, m->sx, s), "cls rows");
+  {
+    DenseCall c;
+    c.flags = EPI_BIAS | EPI_POS | EPI_STATS;
+    c.A = m->u; c.lda = 9 * 64; c.C = m->x; c.ldc = D; c.M = B * P; c.N = D;
+    c.pos = m->pos; c.ldp = D; c.P = P; c.stats_out = m->sx;
+    EVT_RC(dense(m, m->project, c, s));
+  }
+  EVT_RC(run_encoder(m, B, s));  // :127
+  {  // LayerNorm of the CLS rows folded into the classifier (:129-134)
+    DenseCall c;
+    c.flags = EPI_LNIN | EPI_BIAS | EPI_OUT_F32;
+    c.A = m->x; c.lda = (int64_t)T * D; c.C = logits; c.ldc = d.num_classes; c.M = B;
+    c.N = d.num_classes; c.stats_in = m->sx; c.stats_step = T;
+    EVT_RC(dense(m, m->head, c, s));
   }
   return EVT_OK;
 }
@@ -479,6 +731,7 @@ int evt_dense(int dtype, const evt_dense_args* a, void* stream) {
   p.inv_d = a->ln_width > 0 ? 1.0f / (float)a->ln_width : 0.f;
   p.eps = a->ln_eps;
   p.nslots = a->ln_width > 0 ? stats_slots(a->ln_width) : 1;
+  p.stats_step = a->stats_step;
   hipError_t e = gemm_launch(dtype, f, p, (hipStream_t)stream);
   if (e == hipErrorInvalidValue) return fail(EVT_EINVAL, "dense: unsupported flags/shape");
   EVT_HIP(e, "dense");
@@ -511,6 +764,36 @@ int evt_patchify(int dtype, const float* img, int B, int C, int HW, int ps, void
   EVT_HIP(patchify_launch(dtype, img, B, C, HW, ps, out, x, cls, pos, D, stats,
                           (hipStream_t)stream),
           "patchify");
+  return EVT_OK;
+}
+
+int evt_unfold(int dtype, int in_f32, const void* in, int B, int H, int W, int C, int k,
+               int stride, int pad, void* out, int ldo, float* stats, int nslots, void* stream) {
+  if (!in || !out || B < 0 || H <= 0 || W <= 0 || C <= 0 || k <= 0 || stride <= 0 || pad < 0 ||
+      H + 2 * pad < k || W + 2 * pad < k || ldo < k * k * C || (stats && nslots <= 0))
+    return fail(EVT_EINVAL, "unfold: bad shape");
+  if (dtype == EVT_DTYPE_F32 && !in_f32) return fail(EVT_EINVAL, "unfold: f32 path needs f32 input");
+  EVT_HIP(unfold_launch(dtype, in_f32, in, B, H, W, C, k, stride, pad, out, ldo, stats, nslots,
+                        (hipStream_t)stream),
+          "unfold");
+  return EVT_OK;
+}
+
+int64_t evt_performer_scratch(int B, int T) {
+  if (B <= 0 || T <= 0) return 0;
+  return (int64_t)performer_part_floats(B, T);
+}
+
+int evt_performer(int dtype, const void* kqv, int64_t ldq, int B, int T, const float* w,
+                  const float* out_w, const float* out_b, const float* ln2_g, const float* ln2_b,
+                  const float* fc1_w, const float* fc1_b, const float* fc2_w, const float* fc2_b,
+                  float* part, void* out, int64_t ldo, void* stream) {
+  if (!kqv || !w || !out_w || !out_b || !ln2_g || !ln2_b || !fc1_w || !fc1_b || !fc2_w ||
+      !fc2_b || !part || !out || B < 0 || T <= 0 || ldq < 192 || ldo < 64 || ldq % 4 || ldo % 4)
+    return fail(EVT_EINVAL, "performer: bad arguments (ldq >= 192, ldo >= 64, multiples of 4)");
+  PerformerWeights pw{w, out_w, out_b, ln2_g, ln2_b, fc1_w, fc1_b, fc2_w, fc2_b};
+  EVT_HIP(performer_launch(dtype, kqv, ldq, B, T, pw, part, out, ldo, (hipStream_t)stream),
+          "performer");
   return EVT_OK;
 }
 

@@ -43,6 +43,7 @@ struct GemmParams {
   float inv_d;                        // 1 / LayerNorm width
   float eps;                          // LayerNorm epsilon (1e-5)
   int nslots;                         // stats rows are [nslots][2]: per-128-column-slab partials
+  int stats_step;                     // EPI_LNIN: A row m reads stats_in row m * stats_step (0 = 1)
 };
 constexpr int GEMM_BM = 128;
 constexpr int GEMM_BN = 128;
@@ -84,5 +85,29 @@ __host__ __device__ inline int stats_slots(int D) { return 2 * ((D + 255) / 256)
 hipError_t patchify_launch(int dtype, const float* img, int B, int C, int HW, int ps, void* out,
                            void* x, const float* cls, const float* pos, int D, float* stats,
                            hipStream_t s);
+
+// ---- T2T stage (t2t.hip) ----
+struct PerformerWeights {  // fp32 device pointers, Keras layouts
+  const float* prmw;   // [32][64] random-feature matrix (already * sqrt(m))
+  const float* out_w;  // [64][64] attn_output kernel [in][out]
+  const float* out_b;  // [64]
+  const float* ln2_g;  // [64]
+  const float* ln2_b;  // [64]
+  const float* fc1_w;  // [64][64]
+  const float* fc1_b;  // [64]
+  const float* fc2_w;  // [64][64]
+  const float* fc2_b;  // [64]
+};
+// tf_Unfold(k, s, p, channel_last) of NHWC `in` (fp32 if in_f32 else dtype) -> rows [.., ldo].
+hipError_t unfold_launch(int dtype, int in_f32, const void* in, int B, int H, int W, int C, int k,
+                         int s, int p, void* out, int ldo, float* stats, int nslots,
+                         hipStream_t st);
+size_t performer_part_floats(int B, int ntok);
+hipError_t performer_launch(int dtype, const void* kqv, int64_t ldq, int B, int ntok,
+                            const PerformerWeights& w, float* part, void* out, int64_t ldo,
+                            hipStream_t s);
+// CLS rows x[b*ntok] = cls + pos[0] (dtype) and their LayerNorm slot statistics.
+hipError_t cls_rows_launch(int dtype, void* x, int B, int ntok, int D, const float* cls,
+                           const float* pos, float* stats, hipStream_t s);
 
 }  // namespace evt

@@ -140,7 +140,9 @@ __device__ __forceinline__ void epi_rows_t(const GemmParams& p, EVT_LDS char* st
   if (FL & (EPI_LNIN | EPI_RESLN)) {
     const int mr = m0 + row_lo + c;
     if (interior || mr < p.M) {
-      if (FL & EPI_LNIN) ln_coef(p.stats_in, p.nslots, mr, p.inv_d, p.eps, in_mu, in_r);
+      if (FL & EPI_LNIN)
+        ln_coef(p.stats_in, p.nslots, (int64_t)mr * (p.stats_step > 1 ? p.stats_step : 1), p.inv_d,
+                p.eps, in_mu, in_r);
       if (FL & EPI_RESLN) ln_coef(p.rstats, p.nslots, mr, p.inv_d, p.eps, rs_mu, rs_r);
     }
   }
@@ -260,7 +262,9 @@ __device__ __forceinline__ void epi_rows8_t(const GemmParams& p, EVT_LDS char* s
   if (FL & (EPI_LNIN | EPI_RESLN)) {
     const int mr = m0 + row_lo + (lane & 31);
     if (interior || mr < p.M) {
-      if (FL & EPI_LNIN) ln_coef(p.stats_in, p.nslots, mr, p.inv_d, p.eps, in_mu, in_r);
+      if (FL & EPI_LNIN)
+        ln_coef(p.stats_in, p.nslots, (int64_t)mr * (p.stats_step > 1 ? p.stats_step : 1), p.inv_d,
+                p.eps, in_mu, in_r);
       if (FL & EPI_RESLN) ln_coef(p.rstats, p.nslots, mr, p.inv_d, p.eps, rs_mu, rs_r);
     }
   }
@@ -667,6 +671,7 @@ hipError_t dispatch(int flags, const GemmParams& p, hipStream_t s) {
     EVT_CASE(EPI_BIAS | EPI_POS | EPI_STATS)                 // patch embed -> stream + stats
     EVT_CASE(EPI_LNIN | EPI_BIAS)                            // LN1-folded QKV
     EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_GELU)                 // LN2-folded FC1 + GELU
+    EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_OUT_F32)              // LN-folded classifier (T2T)
     EVT_CASE(EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS)   // out-proj / FC2 + LN residual
 #undef EVT_CASE
     default: return hipErrorInvalidValue;

@@ -1,0 +1,444 @@
+// Tokens-to-token (T2T) stage of T2T-ViT on gfx950: soft split (unfold) and TokenPerformer.
+//
+// Reference: `modeling/models/t2t_vit.py:7-88` (tf_Unfold, T2T_module) and
+// `modeling/layers/transformer_encoder.py:39-101` (TokenPerformer). Per performer:
+//
+//   unfold_kernel       NHWC [B,H,W,C] -> rows [B*OH*OW][ldo] in (kh, kw, c) order (extract_patches,
+//                       channel_last), zero padded past k*k*C, + per-row (sum, sumsq) for the
+//                       LayerNorm norm1 that is folded into the kqv GEMM (gemm.hip, EPI_LNIN)
+//   kqv GEMM            (gemm.hip) LN1-folded Dense(3*64) + bias -> [rows][192] = (k | q | v)
+//   performer_kv_kernel per (image, token chunk): kp = prm_exp(k); partial sum_t kp [m] and
+//                       kptv = v^T kp [64][m] (fixed-order, no atomics)
+//   performer_out_kernel per (image, token range): kptv, ksum = fixed-order sum of the chunk
+//                       partials; per token qp = prm_exp(q), D = qp . ksum,
+//                       y = v + Dense(qp kptv^T / (D + 1e-8)), out = y + FFN(LN2(y)) -> [rows][64]
+//
+// The per-token chains in the performer kernels run on MFMA with the operands never leaving
+// registers: products are formed transposed (out^T = W^T in^T), so the 16x16 accumulator of one
+// step (lane l: 4 consecutive features 4(l>>4)+j of token l&15) is exactly the B operand of the
+// next 16x16x16 step (bf16: v_mfma_f32_16x16x16_bf16; f32: 4 x v_mfma_f32_16x16x4_f32 over the
+// same k-permutation). Weights live in LDS as [out][in] fp32 rows with the 16-B chunk q of row r
+// stored at q ^ (r & 15) (conflict-free fragment reads).
+#include "common.h"
+#include "evt_internal.h"
+
+namespace evt {
+
+namespace {
+
+constexpr int PF_HS = 64;  // TokenPerformer head size (token_size)
+constexpr int PF_M = 32;   // random features m = int(64 * 0.5)
+constexpr int PF_PART = PF_HS * PF_M + PF_M;  // floats per (image, chunk) partial: kptv + ksum
+
+// acc[n][col] += sum_{k<16} A[n][k] B[k][col]. Lane l supplies a[s] = A[l&15][4(l>>4)+s] and
+// b[s] = B[4(l>>4)+s][l&15] (s = 0..3): b is a 16x16 accumulator fragment of the previous step.
+template <typename T> __device__ __forceinline__ void chain16(f32x4& acc, const f32x4& a, const f32x4& b);
+template <> __device__ __forceinline__ void chain16<bf16>(f32x4& acc, const f32x4& a, const f32x4& b) {
+  const bf16x4 ah = {(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3]};
+  const bf16x4 bh = {(bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
+  acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(i16x4, ah),
+                                                  __builtin_bit_cast(i16x4, bh), acc, 0, 0, 0);
+}
+template <> __device__ __forceinline__ void chain16<float>(f32x4& acc, const f32x4& a, const f32x4& b) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
+}
+
+// Swizzled fp32 LDS matrix with 64-float rows: element (r, c) at r*64 + (((c>>2) ^ (r&15))<<2) + (c&3).
+__device__ __forceinline__ int swz64(int r, int c) { return r * 64 + ((((c >> 2) ^ (r & 15))) << 2) + (c & 3); }
+
+// A fragment of rows [16*rt, 16*rt+16), k columns [16*kc, 16*kc+16) of a swz64 matrix.
+__device__ __forceinline__ f32x4 afrag(const EVT_LDS float* M, int rt, int kc, int lane) {
+  const int r = 16 * rt + (lane & 15);
+  const int q = 4 * kc + (lane >> 4);
+  return *(const EVT_LDS f32x4*)(M + r * 64 + ((q ^ (r & 15)) << 2));
+}
+
+// Sum over the 4 lanes that hold one token (lanes l, l^16, l^32, l^48).
+__device__ __forceinline__ float token_sum(float v) {
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+template <typename TI, typename TO, bool VEC>
+__global__ __launch_bounds__(256) void unfold_kernel(const TI* __restrict__ in, int B, int H, int W,
+                                                     int C, int k, int s, int p, int OH, int OW,
+                                                     TO* __restrict__ out, int ldo,
+                                                     float* __restrict__ stats, int nslots) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t rows = (int64_t)B * OH * OW;
+  if (row >= rows) return;
+  const int b = (int)(row / (OH * OW)), rem = (int)(row - (int64_t)b * OH * OW);
+  const int oh = rem / OW, ow = rem - oh * OW;
+  const int kc = k * C, kk = k * kc;
+  const TI* img = in + (int64_t)b * H * W * C;
+  TO* orow = out + row * ldo;
+  float s1 = 0.f, s2 = 0.f;
+  if constexpr (VEC) {  // C % 4 == 0: groups of 4 channels never straddle a (kh, kw) pixel
+    for (int e = lane * 4; e < ldo; e += 256) {
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (e < kk) {
+        const int kh = e / kc, r2 = e - kh * kc, kw = r2 / C, c = r2 - kw * C;
+        const int ih = oh * s - p + kh, iw = ow * s - p + kw;
+        if (ih >= 0 && ih < H && iw >= 0 && iw < W) v = load4(img + ((int64_t)ih * W + iw) * C + c);
+      }
+      store4(orow + e, v);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float q = to_f32(from_f32<TO>(v[j]));
+        s1 += q;
+        s2 += q * q;
+      }
+    }
+  } else {
+    for (int e = lane; e < ldo; e += 64) {
+      float v = 0.f;
+      if (e < kk) {
+        const int kh = e / kc, r2 = e - kh * kc, kw = r2 / C, c = r2 - kw * C;
+        const int ih = oh * s - p + kh, iw = ow * s - p + kw;
+        if (ih >= 0 && ih < H && iw >= 0 && iw < W) v = to_f32(img[((int64_t)ih * W + iw) * C + c]);
+      }
+      const TO o = from_f32<TO>(v);
+      orow[e] = o;
+      const float q = to_f32(o);
+      s1 += q;
+      s2 += q * q;
+    }
+  }
+  if (stats) {
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane < nslots) {
+      float* st = stats + 2 * (row * nslots + lane);
+      st[0] = lane == 0 ? s1 : 0.f;
+      st[1] = lane == 0 ? s2 : 0.f;
+    }
+  }
+}
+
+// kp = prm_exp(k) of one 16-token tile: returns the 2 accumulator fragments (m tiles).
+template <typename T>
+__device__ __forceinline__ void prm_tile(const EVT_LDS float* wS, const f32x4 (&z)[4], float zd,
+                                         float inv_sqrt_m, int lane, f32x4 (&out)[2]) {
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) chain16<T>(acc, afrag(wS, mt, c, lane), z[c]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[mt][j] = __expf(acc[j] - zd) * inv_sqrt_m;
+  }
+}
+
+// One token row's 64 features of column block `col0` of the kqv matrix as 4 B fragments.
+template <typename T>
+__device__ __forceinline__ void load_frags(const T* rowp, bool valid, int lane, f32x4 (&f)[4]) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    f[c] = valid ? load4(rowp + 16 * c + 4 * (lane >> 4)) : f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// grid (nchunk, B), block 256 (4 waves; wave w takes tiles w, w+4, ... of the chunk).
+template <typename T>
+__global__ __launch_bounds__(256) void performer_kv_kernel(const T* __restrict__ kqv, int64_t ldq,
+                                                           int ntok, int chunk,
+                                                           const float* __restrict__ prmw,
+                                                           float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float smem[PF_M * 64 + 4 * 2 * 16 * 64 + 4 * PF_PART];
+  EVT_LDS float* wS = (EVT_LDS float*)smem;                    // [32][64] swz64
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  EVT_LDS float* kpS = wS + PF_M * 64 + wave * 2 * 16 * 64;    // [16][64] swz64 (32 used)
+  EVT_LDS float* vS = kpS + 16 * 64;                           // [16][64] swz64
+  EVT_LDS float* red = wS + PF_M * 64 + 4 * 2 * 16 * 64;       // [4][PF_PART]
+  const int b = blockIdx.y, ci = blockIdx.x;
+  for (int i = tid; i < PF_M * PF_HS; i += 256) wS[swz64(i >> 6, i & 63)] = prmw[i];
+  __syncthreads();
+  const int t_lo = ci * chunk, t_hi = min(ntok, t_lo + chunk);
+  const float inv_sqrt_m = 1.0f / sqrtf((float)PF_M);
+  float acc[PF_M];  // kptv[n = lane][m]
+#pragma unroll
+  for (int m = 0; m < PF_M; ++m) acc[m] = 0.f;
+  float ks[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // ksum partial, m = 16mt + 4(l>>4) + j
+  for (int t0 = t_lo + 16 * wave; t0 < t_hi; t0 += 64) {
+    const int t = t0 + (lane & 15);
+    const bool valid = t < t_hi;
+    const T* rowp = kqv + ((int64_t)b * ntok + t) * ldq;
+    f32x4 kf[4], vf[4];
+    load_frags(rowp, valid, lane, kf);           // k = columns [0, 64)   (split order k, q, v)
+    load_frags(rowp + 2 * PF_HS, valid, lane, vf);  // v = columns [128, 192)
+    float kd = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) kd += kf[c][0] * kf[c][0] + kf[c][1] * kf[c][1] + kf[c][2] * kf[c][2] + kf[c][3] * kf[c][3];
+    kd = 0.5f * token_sum(kd);
+    f32x4 kp[2];
+    prm_tile<T>(wS, kf, kd, inv_sqrt_m, lane, kp);
+    const int tr = lane & 15;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      if (!valid) kp[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ks[mt * 4 + j] += kp[mt][j];
+      *(EVT_LDS f32x4*)(kpS + swz64(tr, 16 * mt + 4 * (lane >> 4))) = kp[mt];
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) *(EVT_LDS f32x4*)(vS + swz64(tr, 16 * c + 4 * (lane >> 4))) = vf[c];
+    __builtin_amdgcn_wave_barrier();
+    // kptv[n][m] += sum_t v[t][n] kp[t][m]   (lane = n)
+#pragma unroll 4
+    for (int tt = 0; tt < 16; ++tt) {
+      const float vn = vS[swz64(tt, lane)];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const f32x4 kq = *(const EVT_LDS f32x4*)(kpS + swz64(tt, 4 * q));
+        acc[4 * q + 0] += vn * kq[0];
+        acc[4 * q + 1] += vn * kq[1];
+        acc[4 * q + 2] += vn * kq[2];
+        acc[4 * q + 3] += vn * kq[3];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  // ksum: reduce over the 16 lanes sharing (l >> 4)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) ks[i] += __shfl_xor(ks[i], o, 64);
+  }
+  EVT_LDS float* myred = red + wave * PF_PART;
+#pragma unroll
+  for (int m = 0; m < PF_M; ++m) myred[lane * PF_M + m] = acc[m];
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) myred[PF_HS * PF_M + 16 * mt + 4 * (lane >> 4) + j] = ks[mt * 4 + j];
+  }
+  __syncthreads();
+  float* dst = part + ((int64_t)b * gridDim.x + ci) * PF_PART;
+  for (int i = tid; i < PF_PART; i += 256)
+    dst[i] = ((red[i] + red[PF_PART + i]) + red[2 * PF_PART + i]) + red[3 * PF_PART + i];
+}
+
+// grid (ceil(ntok / span), B), block 256. LDS ~74 KB.
+template <typename T>
+__global__ __launch_bounds__(256) void performer_out_kernel(const T* __restrict__ kqv, int64_t ldq,
+                                                            int ntok, int span,
+                                                            const float* __restrict__ part,
+                                                            int nchunk, PerformerWeights pw,
+                                                            T* __restrict__ out, int64_t ldo) {
+  extern __shared__ __attribute__((aligned(16))) float dsm[];
+  EVT_LDS float* wS = (EVT_LDS float*)dsm;     // [32][64]
+  EVT_LDS float* kvS = wS + PF_M * 64;         // [64][64] (m < 32 used)
+  EVT_LDS float* woS = kvS + 64 * 64;          // [n][k]
+  EVT_LDS float* w1S = woS + 64 * 64;
+  EVT_LDS float* w2S = w1S + 64 * 64;
+  EVT_LDS float* vec = w2S + 64 * 64;          // ksum[64 (32 used)], bo, b1, b2, g2, be2
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.y;
+  for (int i = tid; i < PF_M * PF_HS; i += 256) wS[swz64(i >> 6, i & 63)] = pw.prmw[i];
+  for (int i = tid; i < 64 * 64; i += 256) {
+    const int kr = i >> 6, nc = i & 63;  // Keras [in = kr][out = nc] -> LDS [out][in]
+    woS[swz64(nc, kr)] = pw.out_w[i];
+    w1S[swz64(nc, kr)] = pw.fc1_w[i];
+    w2S[swz64(nc, kr)] = pw.fc2_w[i];
+  }
+  // kptv / ksum of this image: fixed-order sum of the chunk partials
+  const float* pb = part + (int64_t)b * nchunk * PF_PART;
+  for (int i = tid; i < PF_PART; i += 256) {
+    float v = 0.f;
+    for (int c = 0; c < nchunk; ++c) v += pb[(int64_t)c * PF_PART + i];
+    if (i < PF_HS * PF_M) kvS[swz64(i / PF_M, i % PF_M)] = v;
+    else vec[i - PF_HS * PF_M] = v;
+  }
+  for (int i = tid; i < 64; i += 256) {
+    vec[64 + i] = pw.out_b[i];
+    vec[128 + i] = pw.fc1_b[i];
+    vec[192 + i] = pw.fc2_b[i];
+    vec[256 + i] = pw.ln2_g[i];
+    vec[320 + i] = pw.ln2_b[i];
+  }
+  __syncthreads();
+  const float inv_sqrt_m = 1.0f / sqrtf((float)PF_M);
+  const int t_lo = blockIdx.x * span, t_hi = min(ntok, t_lo + span);
+  const int g4 = 4 * (lane >> 4);  // this lane's feature offset inside a 16-feature tile
+  for (int t0 = t_lo + 16 * wave; t0 < t_hi; t0 += 64) {
+    const int t = t0 + (lane & 15);
+    const bool valid = t < t_hi;
+    const T* rowp = kqv + ((int64_t)b * ntok + t) * ldq;
+    f32x4 qf[4], vf[4];
+    load_frags(rowp + PF_HS, valid, lane, qf);
+    load_frags(rowp + 2 * PF_HS, valid, lane, vf);
+    float qd = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) qd += qf[c][0] * qf[c][0] + qf[c][1] * qf[c][1] + qf[c][2] * qf[c][2] + qf[c][3] * qf[c][3];
+    qd = 0.5f * token_sum(qd);
+    f32x4 qp[2];
+    prm_tile<T>(wS, qf, qd, inv_sqrt_m, lane, qp);
+    float dn = 0.f;  // D_t = qp . ksum  (transformer_encoder.py:86)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dn += qp[mt][j] * vec[16 * mt + g4 + j];
+    const float rden = 1.0f / (token_sum(dn) + 1e-8f);
+    f32x4 y[4];  // y^T = kptv . qp^T / (D + eps)   (:88-90)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int mc = 0; mc < 2; ++mc) chain16<T>(acc, afrag(kvS, nt, mc, lane), qp[mc]);
+      y[nt] = acc * rden;
+    }
+    f32x4 y2[4];  // y2 = v + attn_output(y)   (:93)
+    float s1 = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) chain16<T>(acc, afrag(woS, nt, c, lane), y[c]);
+      const f32x4 bo = *(const EVT_LDS f32x4*)(vec + 64 + 16 * nt + g4);
+      y2[nt] = acc + bo + vf[nt];
+      s1 += y2[nt][0] + y2[nt][1] + y2[nt][2] + y2[nt][3];
+    }
+    const float mu = token_sum(s1) * (1.0f / 64.0f);
+    float s2 = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const f32x4 d = y2[nt] - mu;
+      s2 += d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3];
+    }
+    const float rstd = rsqrtf(token_sum(s2) * (1.0f / 64.0f) + 1e-5f);
+    f32x4 hn[4];  // LN2(y2)   (:99 norm2)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const f32x4 g = *(const EVT_LDS f32x4*)(vec + 256 + 16 * nt + g4);
+      const f32x4 be = *(const EVT_LDS f32x4*)(vec + 320 + 16 * nt + g4);
+      hn[nt] = (y2[nt] - mu) * rstd * g + be;
+    }
+    f32x4 h1[4];  // gelu(Dense(64))   (ffn.py:8)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) chain16<T>(acc, afrag(w1S, nt, c, lane), hn[c]);
+      acc += *(const EVT_LDS f32x4*)(vec + 128 + 16 * nt + g4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) h1[nt][j] = gelu_tanh(acc[j]);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {  // out = y2 + Dense(64)(h1)   (ffn.py:9, :99)
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) chain16<T>(acc, afrag(w2S, nt, c, lane), h1[c]);
+      acc += *(const EVT_LDS f32x4*)(vec + 192 + 16 * nt + g4) + y2[nt];
+      if (valid) store4(out + ((int64_t)b * ntok + t) * ldo + 16 * nt + g4, acc);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void cls_rows_kernel(T* __restrict__ x, int ntok, int D,
+                                                      const float* __restrict__ cls,
+                                                      const float* __restrict__ pos,
+                                                      float* __restrict__ stats, int nslots) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int64_t row = (int64_t)b * ntok;
+  float s1 = 0.f, s2 = 0.f;
+  for (int n = lane; n < D; n += 64) {
+    const T v = from_f32<T>(cls[n] + pos[n]);
+    x[row * D + n] = v;
+    const float q = to_f32(v);
+    s1 += q;
+    s2 += q * q;
+  }
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if (stats && lane < nslots) {
+    float* st = stats + 2 * (row * nslots + lane);
+    st[0] = lane == 0 ? s1 : 0.f;
+    st[1] = lane == 0 ? s2 : 0.f;
+  }
+}
+
+template <typename TI, typename TO>
+hipError_t unfold_t(const void* in, int B, int H, int W, int C, int k, int s, int p, void* out,
+                    int ldo, float* stats, int nslots, hipStream_t st) {
+  const int OH = (H + 2 * p - k) / s + 1, OW = (W + 2 * p - k) / s + 1;
+  const int64_t rows = (int64_t)B * OH * OW;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  if (C % 4 == 0 && ldo % 4 == 0)
+    hipLaunchKernelGGL((unfold_kernel<TI, TO, true>), grid, dim3(256), 0, st, (const TI*)in, B, H,
+                       W, C, k, s, p, OH, OW, (TO*)out, ldo, stats, nslots);
+  else
+    hipLaunchKernelGGL((unfold_kernel<TI, TO, false>), grid, dim3(256), 0, st, (const TI*)in, B, H,
+                       W, C, k, s, p, OH, OW, (TO*)out, ldo, stats, nslots);
+  return hipGetLastError();
+}
+
+constexpr size_t PF_OUT_LDS = (size_t)(PF_M * 64 + 4 * 64 * 64 + 6 * 64) * sizeof(float);
+
+template <typename T>
+hipError_t performer_t(const void* kqv, int64_t ldq, int B, int ntok, int chunk, int nchunk,
+                       float* part, const PerformerWeights& w, int span, void* out, int64_t ldo,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(performer_kv_kernel<T>, dim3(nchunk, B), dim3(256), 0, s, (const T*)kqv, ldq,
+                     ntok, chunk, w.prmw, part);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  (void)hipFuncSetAttribute((const void*)performer_out_kernel<T>,
+                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)PF_OUT_LDS);
+  hipLaunchKernelGGL(performer_out_kernel<T>, dim3((ntok + span - 1) / span, B), dim3(256),
+                     PF_OUT_LDS, s, (const T*)kqv, ldq, ntok, span, part, nchunk, w, (T*)out, ldo);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t unfold_launch(int dtype, int in_f32, const void* in, int B, int H, int W, int C, int k,
+                         int s, int p, void* out, int ldo, float* stats, int nslots,
+                         hipStream_t st) {
+  if (B <= 0) return hipSuccess;
+  if (k <= 0 || s <= 0 || p < 0 || H + 2 * p < k || W + 2 * p < k || ldo < k * k * C)
+    return hipErrorInvalidValue;
+  if (dtype == DT_BF16)
+    return in_f32 ? unfold_t<float, bf16>(in, B, H, W, C, k, s, p, out, ldo, stats, nslots, st)
+                  : unfold_t<bf16, bf16>(in, B, H, W, C, k, s, p, out, ldo, stats, nslots, st);
+  return unfold_t<float, float>(in, B, H, W, C, k, s, p, out, ldo, stats, nslots, st);
+}
+
+static int performer_chunks(int ntok) { return (ntok + 783) / 784; }
+
+size_t performer_part_floats(int B, int ntok) {
+  return (size_t)B * performer_chunks(ntok) * PF_PART;
+}
+
+hipError_t performer_launch(int dtype, const void* kqv, int64_t ldq, int B, int ntok,
+                            const PerformerWeights& w, float* part, void* out, int64_t ldo,
+                            hipStream_t s) {
+  if (B <= 0 || ntok <= 0) return hipSuccess;
+  if (ldq < 3 * PF_HS || ldo < PF_HS || (ldq & 3) || (ldo & 3)) return hipErrorInvalidValue;
+  const int nchunk = performer_chunks(ntok);
+  const int chunk = (ntok + nchunk - 1) / nchunk;
+  const int span = 512;  // tokens per output workgroup
+  return dtype == DT_BF16
+             ? performer_t<bf16>(kqv, ldq, B, ntok, chunk, nchunk, part, w, span, out, ldo, s)
+             : performer_t<float>(kqv, ldq, B, ntok, chunk, nchunk, part, w, span, out, ldo, s);
+}
+
+hipError_t cls_rows_launch(int dtype, void* x, int B, int ntok, int D, const float* cls,
+                           const float* pos, float* stats, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  const int ns = stats_slots(D);
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(cls_rows_kernel<bf16>, dim3(B), dim3(64), 0, s, (bf16*)x, ntok, D, cls, pos,
+                       stats, ns);
+  else
+    hipLaunchKernelGGL(cls_rows_kernel<float>, dim3(B), dim3(64), 0, s, (float*)x, ntok, D, cls,
+                       pos, stats, ns);
+  return hipGetLastError();
+}
+
+}  // namespace evt

@@ -134,6 +134,142 @@ def make_vit_params(cfg: ViTConfig, seed: int = 0) -> Dict[str, np.ndarray]:
     return params
 
 
+@dataclass(frozen=True)
+class T2TConfig:
+    """Static shape of a `T2T_ViT` (reference `modeling/models/t2t_vit.py:91-114`).
+
+    Tokens-to-token geometry (t2t_vit.py:50-52,61): soft_split0 k7 s4 p2, soft_split1/2 k3 s2 p1
+    -> S/4, S/8, S/16 token grids; TokenPerformer head size `token_size`, m = token_size / 2
+    random features (kernel_ratio 0.5, transformer_encoder.py:59).
+    """
+
+    image_size: int = 224
+    in_chans: int = 3
+    num_classes: int = 1000
+    dim: int = 384                # hidden_size
+    depth: int = 14
+    heads: int = 6                # num_heads (head size dim / heads = 64)
+    mlp_dim: int = 1152           # int(mlp_ratio * hidden_size) (t2t_vit.py:110)
+    token_size: int = 64
+
+    @property
+    def grids(self) -> tuple:
+        s = self.image_size
+        return (s // 4, s // 8, s // 16)
+
+    @property
+    def num_patches(self) -> int:
+        return (self.image_size // 16) ** 2   # t2t_vit.py:61
+
+    @property
+    def tokens(self) -> int:
+        return self.num_patches + 1
+
+    @property
+    def m(self) -> int:
+        return int(self.token_size * 0.5)
+
+    @property
+    def split_dims(self) -> tuple:
+        """Unfolded vector widths feeding performer1, performer2 and project."""
+        return (49 * self.in_chans, 9 * self.token_size, 9 * self.token_size)
+
+    def gflop_per_image(self) -> float:
+        """Matmul FLOPs (2*MAC) per image: T2T stage + encoder + head."""
+        hs, m = self.token_size, self.m
+        g1, g2, g3 = self.grids
+        f = 0.0
+        for t, din in ((g1 * g1, self.split_dims[0]), (g2 * g2, self.split_dims[1])):
+            f += 2.0 * t * din * 3 * hs                  # kqv
+            f += 2.0 * 2 * t * hs * m                     # prm_exp(k), prm_exp(q)
+            f += 2.0 * 2 * t * hs * m                     # kptv, qp . kptv
+            f += 2.0 * 3 * t * hs * hs                    # attn_output, FFN x2
+        f += 2.0 * g3 * g3 * self.split_dims[2] * self.dim   # project
+        n, d = self.tokens, self.dim
+        f += self.depth * (2.0 * n * d * 3 * d + 2.0 * 2 * n * n * d + 2.0 * n * d * d
+                           + 2.0 * 2 * n * d * self.mlp_dim)
+        f += 2.0 * d * self.num_classes
+        return f / 1e9
+
+
+def t2t_config(hidden_size: int, depth: int, num_heads: int, mlp_ratio: float, *,
+               image_size: int = 224, num_classes: int = 1000, token_size: int = 64,
+               in_channels: int = 3) -> T2TConfig:
+    return T2TConfig(image_size=image_size, in_chans=in_channels, num_classes=num_classes,
+                     dim=hidden_size, depth=depth, heads=num_heads,
+                     mlp_dim=int(mlp_ratio * hidden_size), token_size=token_size)
+
+
+def t2t_param_shapes(cfg: T2TConfig) -> List[tuple]:
+    """Ordered (name, shape) list = the C-ABI weight order of evt_t2t_create (include/evt.h)."""
+    hs, m, d = cfg.token_size, cfg.m, cfg.dim
+    out = []
+    for pre, din in (("p1.", cfg.split_dims[0]), ("p2.", cfg.split_dims[1])):
+        out += [(pre + "ln1_g", (din,)), (pre + "ln1_b", (din,)),
+                (pre + "kqv_w", (din, 3 * hs)), (pre + "kqv_b", (3 * hs,)),
+                (pre + "w", (m, hs)),
+                (pre + "out_w", (hs, hs)), (pre + "out_b", (hs,)),
+                (pre + "ln2_g", (hs,)), (pre + "ln2_b", (hs,)),
+                (pre + "fc1_w", (hs, hs)), (pre + "fc1_b", (hs,)),
+                (pre + "fc2_w", (hs, hs)), (pre + "fc2_b", (hs,))]
+    out += [("project_w", (cfg.split_dims[2], d)), ("project_b", (d,)), ("cls", (d,)),
+            ("pos", (cfg.tokens, d))]
+    for i in range(cfg.depth):
+        inner = cfg.heads * 64
+        out += [(f"l{i}.ln1_g", (d,)), (f"l{i}.ln1_b", (d,)),
+                (f"l{i}.qkv_w", (d, 3 * inner)),
+                (f"l{i}.out_w", (inner, d)), (f"l{i}.out_b", (d,)),
+                (f"l{i}.ln2_g", (d,)), (f"l{i}.ln2_b", (d,)),
+                (f"l{i}.fc1_w", (d, cfg.mlp_dim)), (f"l{i}.fc1_b", (cfg.mlp_dim,)),
+                (f"l{i}.fc2_w", (cfg.mlp_dim, d)), (f"l{i}.fc2_b", (d,))]
+    out += [("norm_g", (d,)), ("norm_b", (d,)), ("head_w", (d, cfg.num_classes)),
+            ("head_b", (cfg.num_classes,))]
+    return out
+
+
+def _orthogonal(rng: np.random.Generator, rows: int, cols: int) -> np.ndarray:
+    """Keras `Orthogonal()` (gain 1) for a [rows, cols] kernel: QR of a Gaussian, sign-fixed."""
+    a = rng.standard_normal((max(rows, cols), min(rows, cols)))
+    q, r = np.linalg.qr(a)
+    q = q * np.sign(np.diag(r))
+    return q.T if rows < cols else q
+
+
+def make_t2t_params(cfg: T2TConfig, seed: int = 0) -> Dict[str, np.ndarray]:
+    """Seeded fp32 parameters for a T2T-ViT (same families as make_vit_params; the performer
+    feature matrix is Orthogonal * sqrt(m) (transformer_encoder.py:60-65) and the position table
+    is the fixed sinusoid (t2t_vit.py:106-107))."""
+    from math import sqrt
+    rng = np.random.Generator(np.random.PCG64(seed))
+    params: Dict[str, np.ndarray] = {}
+    for name, shape in t2t_param_shapes(cfg):
+        leaf = name.split(".")[-1]
+        if leaf == "w":
+            v = _orthogonal(rng, shape[0], shape[1]) * sqrt(shape[0])
+        elif name == "pos":
+            v = _sinusoid(shape[0], shape[1])
+        elif leaf.endswith("_w"):
+            v = _glorot(rng, shape[0], shape[1])
+        elif leaf.endswith("_g"):
+            v = 1.0 + rng.normal(0.0, 0.02, size=shape)
+        elif leaf == "cls":
+            v = rng.normal(0.0, 0.05, size=shape)
+        else:  # biases, LN beta
+            v = rng.normal(0.0, 0.02, size=shape)
+        params[name] = np.ascontiguousarray(v, dtype=np.float32)
+    return params
+
+
+def _sinusoid(n_position: int, d_hid: int) -> np.ndarray:
+    """Fixed sinusoid position table of reference `modeling/layers/embedding.py:4-15`."""
+    pos = np.arange(n_position, dtype=np.float64)[:, None]
+    j = np.arange(d_hid)
+    table = pos / np.power(10000.0, 2 * (j // 2) / d_hid)
+    table[:, 0::2] = np.sin(table[:, 0::2])
+    table[:, 1::2] = np.cos(table[:, 1::2])
+    return table.astype(np.float32)
+
+
 def make_images(batch: int, seed: int = 1, image_size: int = 224, chans: int = 3,
                 layout: str = "NCHW") -> np.ndarray:
     """Seeded N(0,1) fp32 images, the distribution of `tools.py:204` / `utils.py:482`."""

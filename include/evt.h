@@ -138,11 +138,14 @@ typedef struct evt_dense_args {
   float* stats_out;                 /* EVT_EPI_STATS: [rows][S][2], this call's slots written */
   int32_t ln_width;                 /* LayerNorm width (D) for the stats */
   float ln_eps;                     /* LayerNorm epsilon (1e-5 in the reference) */
+  int32_t stats_step;               /* EVT_EPI_LNIN: A row m uses stats_in row m * stats_step
+                                       (0 or 1: consecutive; T: the CLS rows of a token stream) */
 } evt_dense_args;
 
 /* Dense layer on the token matrix: C = epi(A . W) (reference tf.keras.layers.Dense), one of the
  * flag sets 0, 1, 3, 17, 21, 25, 137 (patch embed -> stream), 33 (LN-folded QKV),
- * 35 (LN-folded FC1 + GELU), 197 (out-proj / FC2 + LN residual + stats). */
+ * 35 (LN-folded FC1 + GELU), 49 (LN-folded classifier, fp32 logits), 197 (out-proj / FC2 + LN
+ * residual + stats). */
 int evt_dense(int dtype, const evt_dense_args* args, void* stream);
 
 /* Multi-head attention core (attention.py:20-34): qkv [B*N, ldq] with columns (qkv h d), head
@@ -160,6 +163,64 @@ int evt_layernorm(int dtype, const float* x, int64_t ldx, void* y, int64_t ldy,
  * other S-1 slots of that row zeroed; S from the LayerNorm width D as above). */
 int evt_patchify(int dtype, const float* img, int B, int C, int HW, int ps, void* out, void* x,
                  const float* cls, const float* pos, int D, float* stats, void* stream);
+
+/* ---- T2T-ViT (reference modeling/models/t2t_vit.py) ------------------------------------ */
+
+/* Static shape of a T2T_ViT (t2t_vit.py:91-114; factories get_t2t_vit_{7,10,12,14} :138-148).
+ * tokens_type 'performer' only (:49-59). Soft splits k7s4p2, k3s2p1, k3s2p1 give S/4, S/8 and
+ * S/16 token grids; image_size must be a multiple of 16 with (S/16)^2 + 1 <= 256 tokens. */
+typedef struct evt_t2t_desc {
+  int32_t image_size;   /* S = 224 */
+  int32_t in_chans;     /* 3 */
+  int32_t num_classes;  /* 1000 */
+  int32_t dim;          /* hidden_size: multiple of 64, <= 1024 */
+  int32_t depth;        /* encoder layers */
+  int32_t heads;        /* num_heads; dim / heads must be 64 */
+  int32_t mlp_dim;      /* int(mlp_ratio * hidden_size) */
+  int32_t token_size;   /* TokenPerformer head size; this build requires 64 (m = 32) */
+  int32_t dtype;        /* EVT_DTYPE_* */
+  int32_t max_batch;
+} evt_t2t_desc;
+
+/* Number of fp32 weight tensors evt_t2t_create expects, in order:
+ *   for performer p1 (Din = 49*in_chans) then p2 (Din = 9*token_size):
+ *     ln1_g [Din], ln1_b [Din], kqv_w [Din, 3*hs], kqv_b [3*hs], w [m, hs] (Orthogonal*sqrt(m),
+ *     transformer_encoder.py:60-65), out_w [hs, hs], out_b [hs], ln2_g [hs], ln2_b [hs],
+ *     fc1_w [hs, hs], fc1_b [hs], fc2_w [hs, hs], fc2_b [hs]
+ *   project_w [9*hs, D], project_b [D], cls [D], pos [P+1, D] (the sinusoid table),
+ *   per layer i: the 11 ViT encoder tensors (see evt_vit_num_weights),
+ *   norm_g [D], norm_b [D], head_w [D, C], head_b [C]. */
+int evt_t2t_num_weights(const evt_t2t_desc* desc);
+
+/* Build a T2T-ViT (same ownership rules as evt_vit_create). */
+int evt_t2t_create(const evt_t2t_desc* desc, const float* const* weights, int n_weights,
+                   void* stream, evt_model** out);
+
+/* Forward (T2T_ViT.call, t2t_vit.py:120-135): img fp32 NHWC [batch, S, S, in_chans] ->
+ * logits fp32 [batch, num_classes]. Asynchronous on `stream`. */
+int evt_t2t_forward(evt_model* model, const float* img, int batch, float* logits, void* stream);
+
+/* Bytes of device workspace evt_t2t_create allocates for `batch` images. */
+int evt_t2t_query_workspace(const evt_t2t_desc* desc, int batch, size_t* bytes);
+
+/* tf_Unfold(k, stride, pad, channel_last=True) (t2t_vit.py:7-40): NHWC in [B, H, W, C]
+ * (fp32 when in_f32, else `dtype`) -> out [B*OH*OW, ldo] (dtype), vector order (kh, kw, c) of
+ * tf.image.extract_patches, columns [k*k*C, ldo) zeroed. If stats != NULL, each row's
+ * (sum, sumsq) goes to slot 0 of stats[row][nslots][2] (other slots zeroed). */
+int evt_unfold(int dtype, int in_f32, const void* in, int B, int H, int W, int C, int k,
+               int stride, int pad, void* out, int ldo, float* stats, int nslots, void* stream);
+
+/* TokenPerformer core after its kqv Dense (transformer_encoder.py:83-99): kqv [B*T, ldq]
+ * (columns k | q | v, 64 each) -> out [B*T, ldo] = y + FFN(LN2(y)), y = v + attn_output(
+ * qp kptv^T / (D + 1e-8)). Weights fp32 Keras layouts: w [32, 64], out_w/fc1_w/fc2_w [64, 64],
+ * out_b/ln2_g/ln2_b/fc1_b/fc2_b [64]. `part` is scratch of evt_performer_scratch floats. */
+int evt_performer(int dtype, const void* kqv, int64_t ldq, int B, int T, const float* w,
+                  const float* out_w, const float* out_b, const float* ln2_g, const float* ln2_b,
+                  const float* fc1_w, const float* fc1_b, const float* fc2_w, const float* fc2_b,
+                  float* part, void* out, int64_t ldo, void* stream);
+
+/* fp32 scratch elements evt_performer needs for B images of T tokens. */
+int64_t evt_performer_scratch(int B, int T);
 
 #ifdef __cplusplus
 }

@@ -12,7 +12,7 @@ HEADER = os.path.join(REPO, "include", "evt.h")
 
 def _declared():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(evt_\w+)\(", txt, re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t|const char\*)\s+(evt_\w+)\(", txt, re.M)))
 
 
 @pytest.fixture(scope="module")
@@ -27,7 +27,7 @@ def lib():
 def test_header_and_binding_agree():
     from edgevisiontransformer_amd import _lib
     assert _declared() == sorted(_lib.SIGNATURES)
-    assert len(_declared()) == 14
+    assert len(_declared()) == 21
 
 
 def test_every_declared_symbol_is_exported(lib):
@@ -62,3 +62,24 @@ def test_op_entry_points_validate_before_launch(lib):
     assert lib.evt_layernorm(1, None, 0, None, 0, None, None, 1, 7, 1e-5, None) == _lib.EVT_EINVAL
     assert lib.evt_pack_weight(1, None, None, 1, 1, None, 64, 128, None) == _lib.EVT_EINVAL
     assert lib.evt_dense(1, None, None) == _lib.EVT_EINVAL
+
+
+def test_t2t_host_validation(lib):
+    from edgevisiontransformer_amd import _lib
+    from edgevisiontransformer_amd.weights import t2t_config, t2t_param_shapes
+    d = _lib.evt_t2t_desc(224, 3, 1000, 384, 14, 6, 1152, 64, 1, 256)
+    n = lib.evt_t2t_num_weights(ctypes.byref(d))
+    assert n == len(t2t_param_shapes(t2t_config(384, 14, 6, 3))) == 2 * 13 + 4 + 11 * 14 + 4
+    out = ctypes.c_size_t()
+    assert lib.evt_t2t_query_workspace(ctypes.byref(d), 256, ctypes.byref(out)) == 0
+    assert 0.5e9 < out.value < 3e9
+    for bad, msg in ((_lib.evt_t2t_desc(200, 3, 1000, 384, 14, 6, 1152, 64, 1, 8), b"multiple of 16"),
+                     (_lib.evt_t2t_desc(224, 3, 1000, 384, 14, 5, 1152, 64, 1, 8), b"num_heads"),
+                     (_lib.evt_t2t_desc(224, 3, 1000, 384, 14, 6, 1152, 32, 1, 8), b"token_size")):
+        assert lib.evt_t2t_query_workspace(ctypes.byref(bad), 8, ctypes.byref(out)) == _lib.EVT_EINVAL
+        assert msg in lib.evt_last_error()
+    h = ctypes.c_void_p()
+    assert lib.evt_t2t_create(ctypes.byref(d), None, 0, None, ctypes.byref(h)) == _lib.EVT_EINVAL
+    assert lib.evt_unfold(1, 1, None, 1, 8, 8, 3, 7, 4, 2, None, 147, None, 0, None) == _lib.EVT_EINVAL
+    assert lib.evt_performer(1, None, 192, 1, 16, *([None] * 10), None, 64, None) == _lib.EVT_EINVAL
+    assert lib.evt_performer_scratch(2, 3136) == 2 * 4 * (64 * 32 + 32)

@@ -1,0 +1,142 @@
+"""GPU parity of the T2T-ViT path: soft split (unfold), TokenPerformer core, and the whole model
+against the numpy oracle (oracle/t2t_ref.py) and the golden fixtures.
+
+Tolerances (stated): unfold is a copy, exact in both dtypes (bf16: the same round-to-nearest of
+the same inputs); performer core f32 <= 2e-4 relative to the output scale, bf16 <= 3e-2;
+model logits f32 <= 1e-3 max-abs, bf16 <= 5e-2 max-abs and row cosine >= 0.999.
+The T2T stage itself is "parity unpinned" (no runnable reference): the oracle is a
+restatement of the reference lines; the encoder part is pinned by the reference torch twins.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from edgevisiontransformer_amd import _lib
+from edgevisiontransformer_amd.modeling.models.t2t_vit import T2T_ViT, get_t2t_vit_7
+from edgevisiontransformer_amd.weights import digest, make_images, make_t2t_params, t2t_config
+from oracle import t2t_ref
+from tests import _ops
+from tests.golden.make_golden import T2T_CASES
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _round(a, dtype):
+    t = torch.from_numpy(np.asarray(a, dtype=np.float32))
+    return t.to(_ops.TDT[dtype]).float().numpy().astype(np.float64)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("H,C,k,s,p,in_f32", [(32, 3, 7, 4, 2, 1), (28, 64, 3, 2, 1, 0),
+                                              (14, 64, 3, 2, 1, 0), (9, 5, 3, 2, 1, 1)])
+def test_unfold(gpu, dtype, H, C, k, s, p, in_f32):
+    if dtype == "f32" and not in_f32:
+        in_f32 = 1
+    rng = np.random.default_rng(H * 7 + C)
+    x = rng.standard_normal((3, H, H, C)).astype(np.float32)
+    xin = torch.from_numpy(x).to(gpu)
+    if not in_f32:
+        xin = xin.to(_ops.TDT[dtype])
+        x = _round(x, dtype)
+    ref = t2t_ref.unfold_nhwc(x.astype(np.float64), k, s, p)
+    ref = _round(ref, dtype).reshape(-1, k * k * C)
+    ldo = _ops.round_up(k * k * C, 64)
+    out = torch.full((ref.shape[0], ldo), 7.0, dtype=_ops.TDT[dtype], device=gpu)
+    nslots = 2 * ((k * k * C + 255) // 256)
+    stats = torch.full((ref.shape[0], nslots, 2), 9.0, device=gpu)
+    lib = _lib.load_library()
+    _lib.check(lib.evt_unfold(_lib.DTYPE[dtype], in_f32, _ops._p(xin), 3, H, H, C, k, s, p,
+                              _ops._p(out), ldo, _ops._p(stats), nslots, _ops._s()))
+    torch.cuda.synchronize()
+    got = out.float().cpu().numpy()
+    np.testing.assert_array_equal(got[:, :k * k * C], ref)
+    assert not got[:, k * k * C:].any()
+    st = stats.cpu().numpy().astype(np.float64)
+    np.testing.assert_allclose(st[:, :, 0].sum(1), ref.sum(1), rtol=1e-5, atol=1e-4)
+    np.testing.assert_allclose(st[:, :, 1].sum(1), (ref * ref).sum(1), rtol=1e-5, atol=1e-4)
+    assert not st[:, 1:, :].any()
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("T", [784, 3136, 37])
+def test_performer_core(gpu, dtype, T):
+    cfg = t2t_config(256, 1, 4, 2)
+    P = make_t2t_params(cfg, seed=21)
+    rng = np.random.default_rng(T)
+    B = 2
+    kqv = rng.standard_normal((B, T, 192)).astype(np.float32)
+    kqv = _round(kqv, dtype)
+    ref = t2t_ref.performer_core(kqv, {k: v.astype(np.float64) for k, v in P.items()}, "p1.")
+    d = lambda n: torch.from_numpy(P["p1." + n]).to(gpu)  # noqa: E731
+    ws = {n: d(n) for n in ("w", "out_w", "out_b", "ln2_g", "ln2_b", "fc1_w", "fc1_b", "fc2_w", "fc2_b")}
+    kin = torch.from_numpy(kqv.reshape(B * T, 192).astype(np.float32)).to(gpu).to(_ops.TDT[dtype])
+    out = torch.zeros((B * T, 64), dtype=_ops.TDT[dtype], device=gpu)
+    lib = _lib.load_library()
+    part = torch.empty(int(lib.evt_performer_scratch(B, T)), device=gpu)
+    _lib.check(lib.evt_performer(_lib.DTYPE[dtype], _ops._p(kin), 192, B, T,
+                                 *[_ops._p(ws[n]) for n in ("w", "out_w", "out_b", "ln2_g", "ln2_b",
+                                                            "fc1_w", "fc1_b", "fc2_w", "fc2_b")],
+                                 _ops._p(part), _ops._p(out), 64, _ops._s()))
+    torch.cuda.synchronize()
+    got = out.float().cpu().numpy().reshape(B, T, 64)
+    scale = np.abs(ref).max()
+    err = np.abs(got - ref).max() / scale
+    tol = 2e-4 if dtype == "f32" else 3e-2
+    assert err <= tol, f"performer {dtype} T={T}: rel err {err:.2e} > {tol}"
+
+
+def _t2t_model(name, dtype, gpu):
+    args, batch, pseed, iseed = T2T_CASES[name]
+    h, depth, heads, ratio = args
+    params = make_t2t_params(t2t_config(*args), seed=pseed)
+    m = T2T_ViT(hidden_size=h, depth=depth, num_heads=heads, mlp_ratio=ratio, dtype=dtype,
+                weights=params, device=gpu)
+    img = make_images(batch, seed=iseed, layout="NHWC")
+    return m, img
+
+
+@pytest.mark.parametrize("name", list(T2T_CASES))
+def test_t2t_golden_f32(gpu, name):
+    m, img = _t2t_model(name, "f32", gpu)
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    assert digest([img]) == str(z["image_digest"])
+    out = m(img)
+    err = np.abs(out.astype(np.float64) - z["logits"]).max()
+    assert err <= 1e-3, f"{name}: f32 max-abs {err:.3e}"
+
+
+@pytest.mark.parametrize("name", list(T2T_CASES))
+def test_t2t_golden_bf16(gpu, name):
+    m, img = _t2t_model(name, "bf16", gpu)
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    out = m(img).astype(np.float64)
+    ref = z["logits"]
+    err = np.abs(out - ref).max()
+    cos = ((out * ref).sum(1) / (np.linalg.norm(out, axis=1) * np.linalg.norm(ref, axis=1))).min()
+    assert err <= 5e-2 and cos >= 0.999, f"{name}: bf16 max-abs {err:.3e} cos {cos:.5f}"
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+def test_t2t_batch_independence(gpu, dtype):
+    """Images are independent (no cross-image op in t2t_vit.py:120-135): a 5-image batch equals
+    the per-image results bit for bit."""
+    m = get_t2t_vit_7(dtype=dtype, seed=3, device=gpu, max_batch=5)
+    img = torch.from_numpy(make_images(5, seed=9, layout="NHWC")).to(gpu)
+    full = m(img)
+    for i in range(5):
+        one = m(img[i:i + 1].contiguous())
+        assert torch.equal(one[0], full[i]), f"image {i}"
+
+
+def test_t2t_errors_are_loud(gpu):
+    m = get_t2t_vit_7(dtype="bf16", device=gpu, max_batch=1)
+    with pytest.raises(ValueError):
+        m(np.zeros((1, 3, 224, 224), np.float32))   # NCHW given, NHWC expected
+    with pytest.raises(ValueError):
+        T2T_ViT(hidden_size=256, num_heads=3, device=gpu)
+    with pytest.raises(_lib.EvtError):
+        T2T_ViT(hidden_size=320, depth=1, num_heads=5, device=gpu, max_batch=1)  # head size 64

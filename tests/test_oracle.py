@@ -63,3 +63,48 @@ def test_gelu_is_tanh_approximation():
     x = np.linspace(-6, 6, 101)
     ref = 0.5 * x * (1 + np.tanh(np.sqrt(2 / np.pi) * (x + 0.044715 * x ** 3)))
     np.testing.assert_allclose(vit_ref.gelu(x), ref)
+
+
+# ---- T2T-ViT ------------------------------------------------------------------------------
+
+from edgevisiontransformer_amd.weights import make_t2t_params, t2t_config  # noqa: E402
+from oracle import t2t_ref  # noqa: E402
+from tests.golden.make_golden import T2T_CASES  # noqa: E402
+
+
+@pytest.mark.parametrize("name", list(T2T_CASES))
+def test_t2t_oracle_matches_golden(name):
+    """Encoder part pinned by the reference torch twins; the T2T stage is an independent torch
+    formulation of the same reference lines (parity unpinned for that stage)."""
+    args, batch, pseed, iseed = T2T_CASES[name]
+    z = _load(name)
+    cfg = t2t_config(*args)
+    params = make_t2t_params(cfg, seed=pseed)
+    img = make_images(batch, seed=iseed, image_size=cfg.image_size, layout="NHWC")
+    assert digest(params) == str(z["param_digest"]), "weight generator drifted"
+    assert digest([img]) == str(z["image_digest"]), "image generator drifted"
+    trace = {}
+    out = t2t_ref.t2t_vit_forward(params, cfg, img, trace=trace)
+    assert np.abs(out - z["logits"]).max() < 1e-9
+    np.testing.assert_allclose(trace["split2"][:, :4], z["split2_row0"], atol=1e-10)
+    np.testing.assert_allclose(trace["l0.attn"][:, :4], z["l0_attn_row0"], atol=1e-10)
+
+
+@pytest.mark.parametrize("k,s,p,c", [(7, 4, 2, 3), (3, 2, 1, 64), (3, 2, 1, 5)])
+def test_unfold_vector_order_matches_torch_unfold(k, s, p, c):
+    """tf_Unfold(channel_last=True) == torch unfold on NCHW with (c, kh, kw) -> (kh, kw, c)."""
+    import torch
+    rng = np.random.default_rng(k * 100 + c)
+    x = rng.standard_normal((2, 12, 12, c))
+    ours = t2t_ref.unfold_nhwc(x, k, s, p)
+    cols = torch.nn.functional.unfold(torch.from_numpy(x).permute(0, 3, 1, 2), k, padding=p, stride=s)
+    ref = cols.reshape(2, c, k * k, -1).permute(0, 3, 2, 1).reshape(2, -1, k * k * c).numpy()
+    np.testing.assert_array_equal(ours, ref)
+
+
+def test_sinusoid_table_matches_reference_formula():
+    tab = t2t_ref.sinusoid_table(5, 8)
+    assert tab.dtype == np.float32
+    assert tab[0, 0] == 0.0 and tab[0, 1] == 1.0          # sin(0), cos(0)
+    np.testing.assert_allclose(tab[3, 2], np.sin(3 / 10000 ** (2 / 8)), rtol=1e-6)
+    np.testing.assert_allclose(tab[3, 3], np.cos(3 / 10000 ** (2 / 8)), rtol=1e-6)
