@@ -44,7 +44,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=512, help="images per GPU")
-    ap.add_argument("--model", default="deit_base", choices=["deit_base", "deit_small", "deit_tiny"])
+    ap.add_argument("--model", default="deit_base",
+                    choices=["deit_base", "deit_small", "deit_tiny", "t2t_vit_7", "t2t_vit_10",
+                             "t2t_vit_12", "t2t_vit_14"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-probe", action="store_true", help="skip the per-kernel probe")
@@ -97,18 +99,27 @@ def kernel_probe(dtype: str, M: int, K: int, N: int, iters: int = 20) -> float:
 
 
 def cpu_baseline(model_name: str, budget_s: float) -> dict:
-    from oracle.vit_ref import vit_forward
-    from edgevisiontransformer_amd.weights import make_images, make_vit_params
-    from edgevisiontransformer_amd.modeling.models.vit import _cfg_for as cfg_for
-    cfg = cfg_for(model_name)
-    params = make_vit_params(cfg, seed=0)
+    from edgevisiontransformer_amd.weights import make_images, make_t2t_params, make_vit_params
+    if model_name.startswith("t2t"):
+        from oracle.t2t_ref import t2t_vit_forward as fwd
+        from edgevisiontransformer_amd.modeling.models.t2t_vit import t2t_cfg_for
+        cfg = t2t_cfg_for(model_name)
+        params = make_t2t_params(cfg, seed=0)
+        layout, src = "NHWC", "oracle/t2t_ref.py"
+    else:
+        from oracle.vit_ref import vit_forward as fwd
+        from edgevisiontransformer_amd.modeling.models.vit import _cfg_for as cfg_for
+        cfg = cfg_for(model_name)
+        params = make_vit_params(cfg, seed=0)
+        layout, src = "NCHW", "oracle/vit_ref.py"
+    vit_forward = fwd
     p32 = {k: v.astype(np.float32) for k, v in params.items()}
     try:
         from threadpoolctl import threadpool_info
         cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
     except Exception:
         cores = os.cpu_count() or 1
-    img = make_images(1, seed=99)
+    img = make_images(1, seed=99, layout=layout)
     vit_forward(p32, cfg, img, dtype=np.float32)  # warm BLAS
     n, t0 = 0, time.perf_counter()
     while True:
@@ -119,7 +130,7 @@ def cpu_baseline(model_name: str, budget_s: float) -> dict:
             break
     return {"value": n / el, "unit": "images/s", "cores": int(cores), "kind": "port",
             "sample": f"{n} x {model_name} bs=1 forwards of the numpy fp32 restatement "
-                      f"(oracle/vit_ref.py) in {el:.1f} s; reference TF-CPU path not installable"}
+                      f"({src}) in {el:.1f} s; reference TF-CPU path not installable"}
 
 
 def main():
@@ -133,11 +144,16 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    from edgevisiontransformer_amd.modeling.models import vit as vitmod
-    model = vitmod.build_named(args.model, dtype=args.dtype, seed=0, max_batch=args.batch)
+    t2t = args.model.startswith("t2t")
+    if t2t:
+        from edgevisiontransformer_amd.modeling.models import t2t_vit as mod
+    else:
+        from edgevisiontransformer_amd.modeling.models import vit as mod
+    model = mod.build_named(args.model, dtype=args.dtype, seed=0, max_batch=args.batch)
     B = args.batch
     g = torch.Generator(device="cuda").manual_seed(1000 + rank)
-    img = torch.randn((B, 3, 224, 224), generator=g, device="cuda", dtype=torch.float32)
+    shape = (B, 224, 224, 3) if t2t else (B, 3, 224, 224)   # T2T-ViT is channel-last
+    img = torch.randn(shape, generator=g, device="cuda", dtype=torch.float32)
     logits = torch.empty((B, model.num_classes), device="cuda", dtype=torch.float32)
     gathered = torch.empty((world * B, model.num_classes), device="cuda") if world > 1 else None
 
@@ -170,7 +186,8 @@ def main():
     peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
     roof = None
     if rank == 0 and not args.no_probe:
-        M, K, N = B * model.cfg.tokens, model.cfg.dim, model.cfg.ffn[0]
+        ffn = model.cfg.mlp_dim if t2t else model.cfg.ffn[0]
+        M, K, N = B * model.cfg.tokens, model.cfg.dim, ffn
         t_k = kernel_probe(args.dtype, M, K, N)
         ach = 2.0 * M * N * K / t_k / 1e12
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
@@ -182,12 +199,14 @@ def main():
         cpu = cpu_baseline(args.model, args.cpu_seconds)
     if rank == 0:
         out = {
-            "metric": METRIC, "value": round(imgs_per_s, 2), "unit": "images/s", "n_gpus": world,
+            "metric": METRIC if args.model == "deit_base" else f"images/sec {args.model} bs={B}",
+            "value": round(imgs_per_s, 2), "unit": "images/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic N(0,1) NCHW images resident in HBM; deterministic random-init weights",
-            "config": {"workload": f"{args.model}/16-224 forward, bs={B} per GPU, {args.dtype}",
+            "config": {"workload": f"{args.model}/{'224' if t2t else '16-224'} forward, bs={B} per "
+                                   f"GPU, {args.dtype}",
                        "model": args.model, "global_batch": world * B, "per_gpu_batch": B,
                        "seq_len": model.cfg.tokens, "parallelism": f"dp{world} (batch shard, "
                        "RCCL all-gather of logits)" if world > 1 else "dp1"},
