@@ -770,8 +770,9 @@ int evt_patchify(int dtype, const float* img, int B, int C, int HW, int ps, void
 int evt_unfold(int dtype, int in_f32, const void* in, int B, int H, int W, int C, int k,
                int stride, int pad, void* out, int ldo, float* stats, int nslots, void* stream) {
   if (!in || !out || B < 0 || H <= 0 || W <= 0 || C <= 0 || k <= 0 || stride <= 0 || pad < 0 ||
-      H + 2 * pad < k || W + 2 * pad < k || ldo < k * k * C || (stats && nslots <= 0))
-    return fail(EVT_EINVAL, "unfold: bad shape");
+      H + 2 * pad < k || W + 2 * pad < k || ldo < k * k * C || (stats && nslots <= 0) ||
+      ldo > ((C % 4 == 0 && ldo % 4 == 0) ? 1024 : (ldo % 2 == 0 ? 512 : 256)))
+    return fail(EVT_EINVAL, "unfold: bad shape (ldo <= 256; <= 512 if even; <= 1024 if C % 4 == 0)");
   if (dtype == EVT_DTYPE_F32 && !in_f32) return fail(EVT_EINVAL, "unfold: f32 path needs f32 input");
   EVT_HIP(unfold_launch(dtype, in_f32, in, B, H, W, C, k, stride, pad, out, ldo, stats, nslots,
                         (hipStream_t)stream),

@@ -32,16 +32,30 @@ constexpr int PF_PART = PF_HS * PF_M + PF_M;  // floats per (image, chunk) parti
 
 // acc[n][col] += sum_{k<16} A[n][k] B[k][col]. Lane l supplies a[s] = A[l&15][4(l>>4)+s] and
 // b[s] = B[4(l>>4)+s][l&15] (s = 0..3): b is a 16x16 accumulator fragment of the previous step.
-template <typename T> __device__ __forceinline__ void chain16(f32x4& acc, const f32x4& a, const f32x4& b);
-template <> __device__ __forceinline__ void chain16<bf16>(f32x4& acc, const f32x4& a, const f32x4& b) {
-  const bf16x4 ah = {(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3]};
+// The A fragment comes pre-converted (Afrag<T>): weight fragments are loop-invariant and get
+// hoisted into registers, so the bf16 path keeps them at 2 VGPRs each.
+template <typename T> struct Afrag;
+template <> struct Afrag<bf16> {
+  i16x4 v;
+  Afrag() = default;
+  __device__ __forceinline__ explicit Afrag(const f32x4& a) {
+    const bf16x4 h = {(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3]};
+    v = __builtin_bit_cast(i16x4, h);
+  }
+};
+template <> struct Afrag<float> {
+  f32x4 v;
+  Afrag() = default;
+  __device__ __forceinline__ explicit Afrag(const f32x4& a) : v(a) {}
+};
+template <typename T> __device__ __forceinline__ void chain16(f32x4& acc, const Afrag<T>& a, const f32x4& b);
+template <> __device__ __forceinline__ void chain16<bf16>(f32x4& acc, const Afrag<bf16>& a, const f32x4& b) {
   const bf16x4 bh = {(bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
-  acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(i16x4, ah),
-                                                  __builtin_bit_cast(i16x4, bh), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a.v, __builtin_bit_cast(i16x4, bh), acc, 0, 0, 0);
 }
-template <> __device__ __forceinline__ void chain16<float>(f32x4& acc, const f32x4& a, const f32x4& b) {
+template <> __device__ __forceinline__ void chain16<float>(f32x4& acc, const Afrag<float>& a, const f32x4& b) {
 #pragma unroll
-  for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
+  for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[s], b[s], acc, 0, 0, 0);
 }
 
 // Swizzled fp32 LDS matrix with 64-float rows: element (r, c) at r*64 + (((c>>2) ^ (r&15))<<2) + (c&3).
@@ -61,75 +75,113 @@ __device__ __forceinline__ float token_sum(float v) {
   return v;
 }
 
-template <typename TI, typename TO, bool VEC>
+// One wave per output row, RPW consecutive rows per wave (neighbouring windows overlap, so the
+// input stays cache-resident). Every lane owns VW consecutive output elements per access
+// (VW = 4: 4 channels of one pixel, C % 4 == 0; VW = 2: an element pair, which may straddle a
+// pixel, ldo even; VW = 1 otherwise), decomposed into (kh, kw, c) once per lane; per row only the
+// window origin changes. At most 4 accesses per lane (ldo <= 256 * VW).
+template <typename TI, typename TO, int VW>
 __global__ __launch_bounds__(256) void unfold_kernel(const TI* __restrict__ in, int B, int H, int W,
                                                      int C, int k, int s, int p, int OH, int OW,
                                                      TO* __restrict__ out, int ldo,
-                                                     float* __restrict__ stats, int nslots) {
+                                                     float* __restrict__ stats, int nslots,
+                                                     int rpw) {
+  constexpr int NE = VW == 4 ? 1 : VW;  // independently decomposed elements per access
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int64_t rows = (int64_t)B * OH * OW;
-  if (row >= rows) return;
-  const int b = (int)(row / (OH * OW)), rem = (int)(row - (int64_t)b * OH * OW);
-  const int oh = rem / OW, ow = rem - oh * OW;
   const int kc = k * C, kk = k * kc;
-  const TI* img = in + (int64_t)b * H * W * C;
-  TO* orow = out + row * ldo;
-  float s1 = 0.f, s2 = 0.f;
-  if constexpr (VEC) {  // C % 4 == 0: groups of 4 channels never straddle a (kh, kw) pixel
-    for (int e = lane * 4; e < ldo; e += 256) {
-      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (e < kk) {
-        const int kh = e / kc, r2 = e - kh * kc, kw = r2 / C, c = r2 - kw * C;
-        const int ih = oh * s - p + kh, iw = ow * s - p + kw;
-        if (ih >= 0 && ih < H && iw >= 0 && iw < W) v = load4(img + ((int64_t)ih * W + iw) * C + c);
-      }
-      store4(orow + e, v);
+  int rel[4][NE], ekh[4][NE], ekw[4][NE];
+  bool inw[4][NE], col[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+  for (int i = 0; i < 4; ++i) {
+    col[i] = (lane + 64 * i) * VW < ldo;
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      const int e = (lane + 64 * i) * VW + j;
+      inw[i][j] = e < kk;
+      const int kh = inw[i][j] ? e / kc : 0, r2 = e - kh * kc, kw = inw[i][j] ? r2 / C : 0;
+      ekh[i][j] = kh;
+      ekw[i][j] = kw;
+      rel[i][j] = (kh * W + kw) * C + (r2 - kw * C);
+    }
+  }
+  const int64_t rows = (int64_t)B * OH * OW;
+  const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * rpw;
+  for (int r = 0; r < rpw; ++r) {
+    const int64_t row = row0 + r;
+    if (row >= rows) return;
+    const int b = (int)(row / (OH * OW)), rem = (int)(row - (int64_t)b * OH * OW);
+    const int oh = rem / OW, ow = rem - oh * OW;
+    const int ih0 = oh * s - p, iw0 = ow * s - p;
+    const TI* win = in + (int64_t)b * H * W * C + ((int64_t)ih0 * W + iw0) * C;
+    TO* orow = out + row * ldo;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (!col[i]) continue;
+      const int e = (lane + 64 * i) * VW;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < NE; ++j) {
+        const int ih = ih0 + ekh[i][j], iw = iw0 + ekw[i][j];
+        const bool ok = inw[i][j] && ih >= 0 && ih < H && iw >= 0 && iw < W;
+        if constexpr (VW == 4) {
+          if (ok) v = load4(win + rel[i][j]);
+        } else {
+          v[j] = ok ? to_f32(win[rel[i][j]]) : 0.f;
+        }
+      }
+      if constexpr (VW == 4) {
+        store4(orow + e, v);
+      } else if constexpr (VW == 2) {
+        if constexpr (sizeof(TO) == 2) {
+          const bf16x2 o = {(bf16)v[0], (bf16)v[1]};
+          *(bf16x2*)(orow + e) = o;
+        } else {
+          *(f32x2*)(orow + e) = f32x2{v[0], v[1]};
+        }
+      } else {
+        orow[e] = from_f32<TO>(v[0]);
+      }
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
         const float q = to_f32(from_f32<TO>(v[j]));
         s1 += q;
         s2 += q * q;
       }
     }
-  } else {
-    for (int e = lane; e < ldo; e += 64) {
-      float v = 0.f;
-      if (e < kk) {
-        const int kh = e / kc, r2 = e - kh * kc, kw = r2 / C, c = r2 - kw * C;
-        const int ih = oh * s - p + kh, iw = ow * s - p + kw;
-        if (ih >= 0 && ih < H && iw >= 0 && iw < W) v = to_f32(img[((int64_t)ih * W + iw) * C + c]);
+    if (stats) {
+      s1 = wave_sum(s1);
+      s2 = wave_sum(s2);
+      if (lane < nslots) {
+        float* st = stats + 2 * (row * nslots + lane);
+        st[0] = lane == 0 ? s1 : 0.f;
+        st[1] = lane == 0 ? s2 : 0.f;
       }
-      const TO o = from_f32<TO>(v);
-      orow[e] = o;
-      const float q = to_f32(o);
-      s1 += q;
-      s2 += q * q;
-    }
-  }
-  if (stats) {
-    s1 = wave_sum(s1);
-    s2 = wave_sum(s2);
-    if (lane < nslots) {
-      float* st = stats + 2 * (row * nslots + lane);
-      st[0] = lane == 0 ? s1 : 0.f;
-      st[1] = lane == 0 ? s2 : 0.f;
     }
   }
 }
 
-// kp = prm_exp(k) of one 16-token tile: returns the 2 accumulator fragments (m tiles).
+// kp = prm_exp(k) of one 16-token tile from the random-feature fragments fw (2 m tiles x 4 k
+// chunks): returns the 2 accumulator fragments (m tiles).
 template <typename T>
-__device__ __forceinline__ void prm_tile(const EVT_LDS float* wS, const f32x4 (&z)[4], float zd,
-                                         float inv_sqrt_m, int lane, f32x4 (&out)[2]) {
+__device__ __forceinline__ void prm_tile(const Afrag<T> (&fw)[2][4], const f32x4 (&z)[4], float zd,
+                                         float inv_sqrt_m, f32x4 (&out)[2]) {
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int c = 0; c < 4; ++c) chain16<T>(acc, afrag(wS, mt, c, lane), z[c]);
+    for (int c = 0; c < 4; ++c) chain16<T>(acc, fw[mt][c], z[c]);
 #pragma unroll
     for (int j = 0; j < 4; ++j) out[mt][j] = __expf(acc[j] - zd) * inv_sqrt_m;
   }
+}
+
+template <typename T, int R, int K>
+__device__ __forceinline__ void load_afrags(const EVT_LDS float* M, int lane, Afrag<T> (&f)[R][K]) {
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int k = 0; k < K; ++k) f[r][k] = Afrag<T>(afrag(M, r, k, lane));
 }
 
 // One token row's 64 features of column block `col0` of the kqv matrix as 4 B fragments.
@@ -156,6 +208,8 @@ __global__ __launch_bounds__(256) void performer_kv_kernel(const T* __restrict__
   const int b = blockIdx.y, ci = blockIdx.x;
   for (int i = tid; i < PF_M * PF_HS; i += 256) wS[swz64(i >> 6, i & 63)] = prmw[i];
   __syncthreads();
+  Afrag<T> fw[2][4];
+  load_afrags<T>(wS, lane, fw);
   const int t_lo = ci * chunk, t_hi = min(ntok, t_lo + chunk);
   const float inv_sqrt_m = 1.0f / sqrtf((float)PF_M);
   float acc[PF_M];  // kptv[n = lane][m]
@@ -174,7 +228,7 @@ __global__ __launch_bounds__(256) void performer_kv_kernel(const T* __restrict__
     for (int c = 0; c < 4; ++c) kd += kf[c][0] * kf[c][0] + kf[c][1] * kf[c][1] + kf[c][2] * kf[c][2] + kf[c][3] * kf[c][3];
     kd = 0.5f * token_sum(kd);
     f32x4 kp[2];
-    prm_tile<T>(wS, kf, kd, inv_sqrt_m, lane, kp);
+    prm_tile<T>(fw, kf, kd, inv_sqrt_m, kp);
     const int tr = lane & 15;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
@@ -224,7 +278,7 @@ __global__ __launch_bounds__(256) void performer_kv_kernel(const T* __restrict__
 
 // grid (ceil(ntok / span), B), block 256. LDS ~74 KB.
 template <typename T>
-__global__ __launch_bounds__(256) void performer_out_kernel(const T* __restrict__ kqv, int64_t ldq,
+__global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void performer_out_kernel(const T* __restrict__ kqv, int64_t ldq,
                                                             int ntok, int span,
                                                             const float* __restrict__ part,
                                                             int nchunk, PerformerWeights pw,
@@ -262,6 +316,13 @@ __global__ __launch_bounds__(256) void performer_out_kernel(const T* __restrict_
     vec[320 + i] = pw.ln2_b[i];
   }
   __syncthreads();
+  // all weight fragments in registers for the whole token loop
+  Afrag<T> fw[2][4], fkv[4][2], fo[4][4], f1[4][4], f2[4][4];
+  load_afrags<T>(wS, lane, fw);
+  load_afrags<T>(kvS, lane, fkv);
+  load_afrags<T>(woS, lane, fo);
+  load_afrags<T>(w1S, lane, f1);
+  load_afrags<T>(w2S, lane, f2);
   const float inv_sqrt_m = 1.0f / sqrtf((float)PF_M);
   const int t_lo = blockIdx.x * span, t_hi = min(ntok, t_lo + span);
   const int g4 = 4 * (lane >> 4);  // this lane's feature offset inside a 16-feature tile
@@ -277,7 +338,7 @@ __global__ __launch_bounds__(256) void performer_out_kernel(const T* __restrict_
     for (int c = 0; c < 4; ++c) qd += qf[c][0] * qf[c][0] + qf[c][1] * qf[c][1] + qf[c][2] * qf[c][2] + qf[c][3] * qf[c][3];
     qd = 0.5f * token_sum(qd);
     f32x4 qp[2];
-    prm_tile<T>(wS, qf, qd, inv_sqrt_m, lane, qp);
+    prm_tile<T>(fw, qf, qd, inv_sqrt_m, qp);
     float dn = 0.f;  // D_t = qp . ksum  (transformer_encoder.py:86)
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
@@ -289,7 +350,7 @@ __global__ __launch_bounds__(256) void performer_out_kernel(const T* __restrict_
     for (int nt = 0; nt < 4; ++nt) {
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int mc = 0; mc < 2; ++mc) chain16<T>(acc, afrag(kvS, nt, mc, lane), qp[mc]);
+      for (int mc = 0; mc < 2; ++mc) chain16<T>(acc, fkv[nt][mc], qp[mc]);
       y[nt] = acc * rden;
     }
     f32x4 y2[4];  // y2 = v + attn_output(y)   (:93)
@@ -298,7 +359,7 @@ __global__ __launch_bounds__(256) void performer_out_kernel(const T* __restrict_
     for (int nt = 0; nt < 4; ++nt) {
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int c = 0; c < 4; ++c) chain16<T>(acc, afrag(woS, nt, c, lane), y[c]);
+      for (int c = 0; c < 4; ++c) chain16<T>(acc, fo[nt][c], y[c]);
       const f32x4 bo = *(const EVT_LDS f32x4*)(vec + 64 + 16 * nt + g4);
       y2[nt] = acc + bo + vf[nt];
       s1 += y2[nt][0] + y2[nt][1] + y2[nt][2] + y2[nt][3];
@@ -323,7 +384,7 @@ __global__ __launch_bounds__(256) void performer_out_kernel(const T* __restrict_
     for (int nt = 0; nt < 4; ++nt) {
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int c = 0; c < 4; ++c) chain16<T>(acc, afrag(w1S, nt, c, lane), hn[c]);
+      for (int c = 0; c < 4; ++c) chain16<T>(acc, f1[nt][c], hn[c]);
       acc += *(const EVT_LDS f32x4*)(vec + 128 + 16 * nt + g4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) h1[nt][j] = gelu_tanh(acc[j]);
@@ -332,7 +393,7 @@ __global__ __launch_bounds__(256) void performer_out_kernel(const T* __restrict_
     for (int nt = 0; nt < 4; ++nt) {  // out = y2 + Dense(64)(h1)   (ffn.py:9, :99)
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int c = 0; c < 4; ++c) chain16<T>(acc, afrag(w2S, nt, c, lane), h1[c]);
+      for (int c = 0; c < 4; ++c) chain16<T>(acc, f2[nt][c], h1[c]);
       acc += *(const EVT_LDS f32x4*)(vec + 192 + 16 * nt + g4) + y2[nt];
       if (valid) store4(out + ((int64_t)b * ntok + t) * ldo + 16 * nt + g4, acc);
     }
@@ -368,13 +429,17 @@ hipError_t unfold_t(const void* in, int B, int H, int W, int C, int k, int s, in
                     int ldo, float* stats, int nslots, hipStream_t st) {
   const int OH = (H + 2 * p - k) / s + 1, OW = (W + 2 * p - k) / s + 1;
   const int64_t rows = (int64_t)B * OH * OW;
-  const dim3 grid((unsigned)((rows + 3) / 4));
-  if (C % 4 == 0 && ldo % 4 == 0)
-    hipLaunchKernelGGL((unfold_kernel<TI, TO, true>), grid, dim3(256), 0, st, (const TI*)in, B, H,
-                       W, C, k, s, p, OH, OW, (TO*)out, ldo, stats, nslots);
-  else
-    hipLaunchKernelGGL((unfold_kernel<TI, TO, false>), grid, dim3(256), 0, st, (const TI*)in, B, H,
-                       W, C, k, s, p, OH, OW, (TO*)out, ldo, stats, nslots);
+  const int vw = (C % 4 == 0 && ldo % 4 == 0) ? 4 : (ldo % 2 == 0 ? 2 : 1);
+  if (ldo > 256 * vw) return hipErrorInvalidValue;  // <= 4 accesses per lane
+  const int rpw = 4;
+  const dim3 grid((unsigned)((rows + 4 * rpw - 1) / (4 * rpw)));
+#define EVT_UNFOLD(V)                                                                          \
+  hipLaunchKernelGGL((unfold_kernel<TI, TO, V>), grid, dim3(256), 0, st, (const TI*)in, B, H, W, \
+                     C, k, s, p, OH, OW, (TO*)out, ldo, stats, nslots, rpw)
+  if (vw == 4) EVT_UNFOLD(4);
+  else if (vw == 2) EVT_UNFOLD(2);
+  else EVT_UNFOLD(1);
+#undef EVT_UNFOLD
   return hipGetLastError();
 }
 

@@ -205,7 +205,8 @@ int evt_t2t_query_workspace(const evt_t2t_desc* desc, int batch, size_t* bytes);
 
 /* tf_Unfold(k, stride, pad, channel_last=True) (t2t_vit.py:7-40): NHWC in [B, H, W, C]
  * (fp32 when in_f32, else `dtype`) -> out [B*OH*OW, ldo] (dtype), vector order (kh, kw, c) of
- * tf.image.extract_patches, columns [k*k*C, ldo) zeroed. If stats != NULL, each row's
+ * tf.image.extract_patches, columns [k*k*C, ldo) zeroed (ldo <= 256; <= 512 when ldo is even;
+ * <= 1024 when C % 4 == 0 and ldo % 4 == 0). If stats != NULL, each row's
  * (sum, sumsq) goes to slot 0 of stats[row][nslots][2] (other slots zeroed). */
 int evt_unfold(int dtype, int in_f32, const void* in, int B, int H, int W, int C, int k,
                int stride, int pad, void* out, int ldo, float* stats, int nslots, void* stream);
