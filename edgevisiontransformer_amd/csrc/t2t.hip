@@ -104,16 +104,25 @@ __global__ __launch_bounds__(256) void unfold_kernel(const TI* __restrict__ in, 
       rel[i][j] = (kh * W + kw) * C + (r2 - kw * C);
     }
   }
-  const int64_t rows = (int64_t)B * OH * OW;
-  const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * rpw;
-  for (int r = 0; r < rpw; ++r) {
-    const int64_t row = row0 + r;
+  const int rows = B * OH * OW;  // < 2^31 (checked on the host)
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * rpw;
+  if (row0 >= rows) return;
+  // window of the first row, then stepped (no per-row integer division)
+  int b = row0 / (OH * OW), rem = row0 - b * OH * OW;
+  int oh = rem / OW, ow = rem - oh * OW;
+  for (int r = 0; r < rpw; ++r, ++ow) {
+    const int row = row0 + r;
     if (row >= rows) return;
-    const int b = (int)(row / (OH * OW)), rem = (int)(row - (int64_t)b * OH * OW);
-    const int oh = rem / OW, ow = rem - oh * OW;
+    if (ow == OW) {
+      ow = 0;
+      if (++oh == OH) {
+        oh = 0;
+        ++b;
+      }
+    }
     const int ih0 = oh * s - p, iw0 = ow * s - p;
     const TI* win = in + (int64_t)b * H * W * C + ((int64_t)ih0 * W + iw0) * C;
-    TO* orow = out + row * ldo;
+    TO* orow = out + (int64_t)row * ldo;
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -153,7 +162,7 @@ __global__ __launch_bounds__(256) void unfold_kernel(const TI* __restrict__ in, 
       s1 = wave_sum(s1);
       s2 = wave_sum(s2);
       if (lane < nslots) {
-        float* st = stats + 2 * (row * nslots + lane);
+        float* st = stats + 2 * ((int64_t)row * nslots + lane);
         st[0] = lane == 0 ? s1 : 0.f;
         st[1] = lane == 0 ? s2 : 0.f;
       }
@@ -429,6 +438,7 @@ hipError_t unfold_t(const void* in, int B, int H, int W, int C, int k, int s, in
                     int ldo, float* stats, int nslots, hipStream_t st) {
   const int OH = (H + 2 * p - k) / s + 1, OW = (W + 2 * p - k) / s + 1;
   const int64_t rows = (int64_t)B * OH * OW;
+  if (rows >= (int64_t)1 << 31) return hipErrorInvalidValue;
   const int vw = (C % 4 == 0 && ldo % 4 == 0) ? 4 : (ldo % 2 == 0 ? 2 : 1);
   if (ldo > 256 * vw) return hipErrorInvalidValue;  // <= 4 accesses per lane
   const int rpw = 4;
