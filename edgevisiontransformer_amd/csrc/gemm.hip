@@ -186,7 +186,7 @@ __device__ __forceinline__ void epi_rows_t(const GemmParams& p, EVT_LDS char* st
     }
     if (ok) {
       TO* cp = (TO*)p.C + orow * p.ldc + n;
-      if (full) store4(cp, v);
+      if (full) store4_nt(cp, v);
       else
         for (int j = 0; j < 4; ++j)
           if (n + j < p.N) cp[j] = from_f32<TO>(v[j]);
@@ -332,7 +332,7 @@ __device__ __forceinline__ void epi_rows8_t(const GemmParams& p, EVT_LDS char* s
                       (bf16)v[1][0], (bf16)v[1][1], (bf16)v[1][2], (bf16)v[1][3]};
     if (ok) {
       bf16* cp = (bf16*)p.C + orow * p.ldc + n;
-      if (full) *(u32x4*)cp = __builtin_bit_cast(u32x4, o);
+      if (full) __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), (u32x4*)cp);
       else
 #pragma unroll
         for (int j = 0; j < 8; ++j)
