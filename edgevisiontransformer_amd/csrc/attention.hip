@@ -29,8 +29,8 @@ namespace evt {
 
 namespace {
 
-template <int NKT>  // 16-key tiles (keys padded to NKT*16, multiple of 32)
-__global__ __launch_bounds__(256) void attn_bf16_kernel(AttnParams p) {
+template <int NKT>  // 16-key tiles (keys padded to NKT*16; odd NKT: a half last PV step)
+__global__ __launch_bounds__(256, NKT == 13 ? 3 : 1) void attn_bf16_kernel(AttnParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NP = NKT * 16;
   constexpr int ROWB = 128;  // 64 bf16
@@ -40,7 +40,20 @@ __global__ __launch_bounds__(256) void attn_bf16_kernel(AttnParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x / p.H, h = blockIdx.x - b * p.H;
   const bf16* qkv = (const bf16*)p.qkv + (int64_t)b * p.N * p.ldq;
+  const int g = lane >> 4, c16 = lane & 15, sw = lane & 7;
+  const int nqt = (p.N + 15) >> 4;
 
+  // ---- Q fragments of all this wave's query tiles (wave, wave+4, ...), issued together with
+  // the K/V staging so that every load latency overlaps (NQW = max tiles per wave)
+  constexpr int NQW = (NP / 16 + 3) / 4;
+  u32x4 qf[NQW][2];
+#pragma unroll
+  for (int i = 0; i < NQW; ++i) {
+    const int qi = min((wave + 4 * i) * 16 + c16, p.N - 1);
+    const bf16* qrow = qkv + (int64_t)qi * p.ldq + h * 64;
+    qf[i][0] = *(const u32x4*)(qrow + 8 * g);
+    qf[i][1] = *(const u32x4*)(qrow + 8 * (g + 4));
+  }
   // ---- stage K, V (8 rows of 128 B per wave-instruction) ----
   {
     const int srow = lane >> 3, sslot = lane & 7;
@@ -55,13 +68,12 @@ __global__ __launch_bounds__(256) void attn_bf16_kernel(AttnParams p) {
     __syncthreads();
   }
 
-  const int g = lane >> 4, c16 = lane & 15, sw = lane & 7;
-  const int nqt = (p.N + 15) >> 4;
-  for (int qt = wave; qt < nqt; qt += 4) {
-    const int qi = min(qt * 16 + c16, p.N - 1);
-    const bf16* qrow = qkv + (int64_t)qi * p.ldq + h * 64;
-    const u32x4 qf0 = *(const u32x4*)(qrow + 8 * g);
-    const u32x4 qf1 = *(const u32x4*)(qrow + 8 * (g + 4));
+#pragma unroll
+  for (int it = 0; it < NQW; ++it) {
+    const int qt = wave + 4 * it;
+    if (qt >= nqt) break;
+    const u32x4 qf0 = qf[it][0];
+    const u32x4 qf1 = qf[it][1];
 
     f32x4 s[NKT];
 #pragma unroll
@@ -130,13 +142,35 @@ __global__ __launch_bounds__(256) void attn_bf16_kernel(AttnParams p) {
                                                         0, 0, 0);
       }
     }
+    if constexpr (NKT % 2) {  // last 16 keys: the upper k half of the MFMA is zero
+      bf16x8 pf;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pf[j] = (bf16)s[NKT - 1][j];
+        pf[4 + j] = (bf16)0.f;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const int key0 = (NKT - 1) * 16 + 4 * g + tq;
+      const int ksw = key0 & 7;
+      const i16x4 z = {0, 0, 0, 0};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int chunk = 2 * dt + (tp >> 1);
+        const int off = ((chunk ^ ksw) * 16) + (tp & 1) * 8;
+        const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (EVT_LDS i16x4*)(Vs + key0 * ROWB + off));
+        const i16x8 vv = __builtin_shufflevector(v0, z, 0, 1, 2, 3, 4, 5, 6, 7);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[dt],
+                                                        0, 0, 0);
+      }
+    }
     // o[dt][j] = O^T[d = dt*16 + 4g + j][query]
     const int q = qt * 16 + c16;
     if (q < p.N) {
       const float inv = 1.0f / sum;
       bf16* op = (bf16*)p.out + ((int64_t)b * p.N + q) * p.ldo + h * 64 + 4 * g;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) store4(op + dt * 16, o[dt] * inv);
+      for (int dt = 0; dt < 4; ++dt) store4_nt(op + dt * 16, o[dt] * inv);
     }
   }
 }
@@ -247,8 +281,10 @@ hipError_t launch_nkt(int dtype, const AttnParams& p, hipStream_t s) {
   const size_t lds = 2 * (size_t)NKT * 16 * rowb;
   if (dtype == DT_BF16)
     hipLaunchKernelGGL(attn_bf16_kernel<NKT>, dim3(p.B * p.H), dim3(256), lds, s, p);
-  else
+  else if constexpr (NKT % 2 == 0)
     hipLaunchKernelGGL(attn_f32_kernel<NKT>, dim3(p.B * p.H), dim3(256), lds, s, p);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
@@ -271,6 +307,7 @@ hipError_t attention_launch(int dtype, const AttnParams& p, hipStream_t s) {
   set_lds_attrs();
   if (p.N <= 64) return launch_nkt<4>(dtype, p, s);
   if (p.N <= 128) return launch_nkt<8>(dtype, p, s);
+  if (dtype == DT_BF16 && p.N <= 208) return launch_nkt<13>(dtype, p, s);  // 3 blocks per CU (LDS)
   if (p.N <= 224) return launch_nkt<14>(dtype, p, s);
   return launch_nkt<16>(dtype, p, s);
 }
