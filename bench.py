@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-probe", action="store_true", help="skip the per-kernel probe")
+    ap.add_argument("--probe-only", type=int, default=0, metavar="N",
+                    help="only launch the FC1 probe kernel N times and exit (PMC collection)")
     return ap.parse_args()
 
 
@@ -133,6 +135,23 @@ def cpu_baseline(model_name: str, budget_s: float) -> dict:
                       f"({src}) in {el:.1f} s; reference TF-CPU path not installable"}
 
 
+def pmc_traffic(M: int, K: int, N: int):
+    """HBM bytes per launch of the probe kernel from the committed rocprofv3 PMC summary
+    (scripts/gpu_pmc_fc1.sh -> profiles/*_pmc_fc1.json): 2 x FETCH_SIZE (gfx950 tallies 128-B
+    requests at 64 B, MI355X_MICROARCH.md HBM section) + WRITE_SIZE. None if absent or shape differs."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_fc1.json")))
+    if not files:
+        return None
+    try:
+        d = json.load(open(files[-1]))
+    except Exception:
+        return None
+    if (d.get("M"), d.get("K"), d.get("N")) != (M, K, N):
+        return None
+    return d.get("traffic_bytes_per_launch")
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -144,6 +163,13 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
+    if args.probe_only:
+        from edgevisiontransformer_amd.modeling.models.vit import _cfg_for
+        cfg = _cfg_for(args.model)
+        t = kernel_probe(args.dtype, args.batch * cfg.tokens, cfg.dim, cfg.ffn[0], iters=args.probe_only)
+        print(json.dumps({"probe_us": round(t * 1e6, 1), "M": args.batch * cfg.tokens, "K": cfg.dim,
+                          "N": cfg.ffn[0]}), flush=True)
+        return
     t2t = args.model.startswith("t2t")
     if t2t:
         from edgevisiontransformer_amd.modeling.models import t2t_vit as mod
@@ -191,7 +217,7 @@ def main():
         t_k = kernel_probe(args.dtype, M, K, N)
         ach = 2.0 * M * N * K / t_k / 1e12
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(ach / peak, 4), "traffic": None,
+                "frac": round(ach / peak, 4), "traffic": pmc_traffic(M, K, N),
                 "kernel": f"gemm_big_kernel<LNIN|BIAS|GELU> (FC1, {args.dtype}) M={M} K={K} N={N}",
                 "avg_launch_us": round(t_k * 1e6, 1)}
     cpu = None

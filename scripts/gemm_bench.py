@@ -37,6 +37,12 @@ for name, (K, N, fl) in shapes.items():
     _lib.check(lib.evt_pack_weight(1, P(W), ctypes.c_void_p(0), K, N, P(wp), K, npad, S()))
     bias = torch.randn(npad, generator=g, device="cuda") * 0.1
     R = torch.randn((M, N), generator=g, device="cuda").bfloat16()
+    nsl = 2 * ((K + 255) // 256)
+    stats = torch.zeros((M, nsl, 2), device="cuda")   # include/evt.h slot layout
+    Af = A.float()
+    stats[:, 0, 0], stats[:, 0, 1] = Af.sum(1), (Af * Af).sum(1)
+    del Af
+    colsum = torch.randn(npad, generator=g, device="cuda")
     outs = {}
     for v in VARS:
         outs[v] = torch.empty((M, N + LDC_PAD), dtype=torch.float32 if fl & 16 else torch.bfloat16,
@@ -48,6 +54,8 @@ for name, (K, N, fl) in shapes.items():
         a.C, a.ldc, a.M, a.N, a.bias = outs[v].data_ptr(), N + LDC_PAD, M, N, bias.data_ptr()
         if fl & 4:
             a.resid, a.ldr = R.data_ptr(), N
+        if fl & 32:
+            a.colsum, a.stats_in, a.ln_width, a.ln_eps = colsum.data_ptr(), stats.data_ptr(), K, 1e-5
         _lib.check(lib.evt_dense(1, ctypes.byref(a), S()))
     times = {v: [] for v in VARS}
     for v in VARS:
