@@ -76,6 +76,8 @@ SIGNATURES = {
     "evt_vit_forward": (_I, [_P, _P, _I, _P, _P]),
     "evt_query_workspace": (_I, [ctypes.POINTER(evt_vit_desc), _I, ctypes.POINTER(ctypes.c_size_t)]),
     "evt_model_destroy": (_I, [_P]),
+    "evt_graph_capture": (_I, [_P, _P, _I, _P, _P]),
+    "evt_graph_launch": (_I, [_P, _P]),
     "evt_set_gemm_variant": (_I, [_I]),
     "evt_pack_weight": (_I, [_I, _P, _P, _I, _I, _P, _I, _I, _P]),
     "evt_ln_fold": (_I, [_I, _P, _I, _I, _P, _P, _P, _I, _I, _P, _P, _P]),

@@ -112,6 +112,8 @@ struct evt_model {
   void* hbuf = nullptr;      // [B*T, ffn_st]
   void* hh = nullptr;        // [B, head_st]
   size_t ws_bytes = 0;
+  hipGraph_t graph = nullptr;        // evt_graph_capture
+  hipGraphExec_t graph_exec = nullptr;
 };
 
 namespace {
@@ -447,6 +449,8 @@ int evt_query_workspace(const evt_vit_desc* desc, int batch, size_t* bytes) {
 
 int evt_model_destroy(evt_model* m) {
   if (!m) return EVT_OK;
+  if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
+  if (m->graph) (void)hipGraphDestroy(m->graph);
   for (void* p : m->allocs) (void)hipFree(p);
   delete m;
   return EVT_OK;
@@ -673,6 +677,44 @@ int evt_t2t_forward(evt_model* m, const float* img, int B, float* logits, void* 
     c.N = d.num_classes; c.stats_in = m->sx; c.stats_step = T;
     EVT_RC(dense(m, m->head, c, s));
   }
+  return EVT_OK;
+}
+
+int evt_graph_capture(evt_model* m, const float* img, int batch, float* logits, void* stream) {
+  if (!m || !stream) return fail(EVT_EINVAL, "graph capture needs a model and a non-NULL stream");
+  hipStream_t s = (hipStream_t)stream;
+  if (m->graph_exec) {
+    (void)hipGraphExecDestroy(m->graph_exec);
+    m->graph_exec = nullptr;
+  }
+  if (m->graph) {
+    (void)hipGraphDestroy(m->graph);
+    m->graph = nullptr;
+  }
+  EVT_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal), "begin capture");
+  const int rc = m->family == 0 ? evt_vit_forward(m, img, batch, logits, stream)
+                                : evt_t2t_forward(m, img, batch, logits, stream);
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(s, &g);
+  if (rc) {
+    if (g) (void)hipGraphDestroy(g);
+    return rc;
+  }
+  if (e != hipSuccess) return hip_fail(e, "end capture");
+  hipGraphExec_t ge = nullptr;
+  const hipError_t ei = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+  if (ei != hipSuccess) {
+    (void)hipGraphDestroy(g);
+    return hip_fail(ei, "graph instantiate");
+  }
+  m->graph = g;
+  m->graph_exec = ge;
+  return EVT_OK;
+}
+
+int evt_graph_launch(evt_model* m, void* stream) {
+  if (!m || !m->graph_exec) return fail(EVT_EINVAL, "no captured graph (call evt_graph_capture)");
+  EVT_HIP(hipGraphLaunch(m->graph_exec, (hipStream_t)stream), "graph launch");
   return EVT_OK;
 }
 

@@ -25,7 +25,7 @@ import torch
 
 from ... import _lib
 from ...weights import T2TConfig, make_t2t_params, t2t_config, t2t_param_shapes
-from .vit import _to_device_image
+from .vit import _capture_graph, _replay_graph, _to_device_image
 
 
 class T2T_ViT:
@@ -75,6 +75,7 @@ class T2T_ViT:
     def _build(self, max_batch: int) -> None:
         lib = _lib.load_library()
         self.close()
+        self._graph_io = None
         desc = self._desc(max_batch)
         n = lib.evt_t2t_num_weights(ctypes.byref(desc))
         ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in self._weights])
@@ -114,6 +115,13 @@ class T2T_ViT:
                                        b, ctypes.c_void_p(logits.data_ptr()),
                                        ctypes.c_void_p(_lib.stream_ptr(self.device))))
         return logits
+
+    def capture_graph(self, img: torch.Tensor, logits: torch.Tensor) -> None:
+        """HIP graph of one forward of (img, logits); see ViT.capture_graph."""
+        _capture_graph(self, img, logits)
+
+    def replay_graph(self) -> None:
+        _replay_graph(self)
 
     def __call__(self, img: Union[torch.Tensor, np.ndarray]):
         x, was_numpy = _to_device_image(img, self.device)

@@ -64,6 +64,29 @@ def _to_device_image(img, device) -> Tuple[torch.Tensor, bool]:
     return img.contiguous(), False
 
 
+def _capture_graph(model, img: torch.Tensor, logits: torch.Tensor) -> None:
+    b = img.shape[0]
+    if b > model._max_batch:
+        model._build(b)
+    lib = _lib.load_library()
+    stream = torch.cuda.Stream(model.device)  # capture needs a non-default stream
+    stream.wait_stream(torch.cuda.current_stream(model.device))
+    with torch.cuda.stream(stream):
+        _lib.check(lib.evt_graph_capture(ctypes.c_void_p(model._handle),
+                                         ctypes.c_void_p(img.data_ptr()), b,
+                                         ctypes.c_void_p(logits.data_ptr()),
+                                         ctypes.c_void_p(stream.cuda_stream)))
+    torch.cuda.current_stream(model.device).wait_stream(stream)
+    model._graph_io = (img, logits, b)  # keep the captured buffers alive
+
+
+def _replay_graph(model) -> None:
+    if not getattr(model, "_graph_io", None):
+        raise RuntimeError("no captured graph: call capture_graph(img, logits) first")
+    _lib.check(_lib.load_library().evt_graph_launch(
+        ctypes.c_void_p(model._handle), ctypes.c_void_p(_lib.stream_ptr(model.device))))
+
+
 class ViT:
     """Vision Transformer forward on MI355X (reference `ViT`, vit.py:9-55)."""
 
@@ -115,6 +138,7 @@ class ViT:
     def _build(self, max_batch: int) -> None:
         lib = _lib.load_library()
         self.close()
+        self._graph_io = None
         desc = self._desc(max_batch)
         n = lib.evt_vit_num_weights(ctypes.byref(desc))
         ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in self._weights])
@@ -154,6 +178,15 @@ class ViT:
                                        b, ctypes.c_void_p(logits.data_ptr()),
                                        ctypes.c_void_p(_lib.stream_ptr(self.device))))
         return logits
+
+    # -- HIP graph ----------------------------------------------------------------------------
+    def capture_graph(self, img: torch.Tensor, logits: torch.Tensor) -> None:
+        """Record one forward of the device buffers (img, logits) as a HIP graph
+        (evt_graph_capture); replay_graph() re-runs it after the caller refills img in place."""
+        _capture_graph(self, img, logits)
+
+    def replay_graph(self) -> None:
+        _replay_graph(self)
 
     def __call__(self, img: Union[torch.Tensor, np.ndarray]):
         x, was_numpy = _to_device_image(img, self.device)

@@ -85,6 +85,14 @@ int evt_vit_create(const evt_vit_desc* desc, const float* const* weights, int n_
  * logits fp32 [batch, num_classes]. Asynchronous on `stream`. batch <= max_batch. */
 int evt_vit_forward(evt_model* model, const float* img, int batch, float* logits, void* stream);
 
+/* HIP graph of one forward (either family): captures evt_vit_forward / evt_t2t_forward of
+ * (img, batch, logits) on `stream` (must be a non-NULL stream not being captured) into a graph
+ * owned by the model, replacing any previous one; evt_graph_launch replays it on `stream`
+ * (same pointers, same batch: the caller refills img in place). Removes the per-kernel launch
+ * cost of the ~80-launch forward at small batch. */
+int evt_graph_capture(evt_model* model, const float* img, int batch, float* logits, void* stream);
+int evt_graph_launch(evt_model* model, void* stream);
+
 /* Bytes of device workspace evt_vit_create allocates for `batch` images. */
 int evt_query_workspace(const evt_vit_desc* desc, int batch, size_t* bytes);
 

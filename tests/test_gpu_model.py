@@ -108,3 +108,21 @@ def test_errors_are_loud(gpu):
         ViT(image_size=225, patch_size=16)
     with pytest.raises(EvtError):
         ViT(dim=96, heads=1, mlp_dim=96, depth=1, device=gpu, max_batch=1)  # dim % 64 != 0
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+def test_graph_replay_matches_eager(gpu, dtype):
+    """evt_graph_capture / evt_graph_launch: the replayed HIP graph gives the eager logits bit
+    for bit, and follows in-place updates of the captured input buffer."""
+    m = get_deit_tiny(dtype=dtype, seed=5, device=gpu, max_batch=3)
+    img = torch.from_numpy(make_images(3, seed=21)).to(gpu)
+    eager = m(img).clone()
+    logits = torch.empty_like(eager)
+    m.capture_graph(img, logits)
+    m.replay_graph()
+    torch.cuda.synchronize()
+    assert torch.equal(logits, eager)
+    img.copy_(torch.from_numpy(make_images(3, seed=22)).to(gpu))
+    m.replay_graph()
+    torch.cuda.synchronize()
+    assert torch.equal(logits, m(img))
