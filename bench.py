@@ -218,7 +218,7 @@ def main():
         ach = 2.0 * M * N * K / t_k / 1e12
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(ach / peak, 4), "traffic": pmc_traffic(M, K, N),
-                "kernel": f"gemm_big_kernel<LNIN|BIAS|GELU> (FC1, {args.dtype}) M={M} K={K} N={N}",
+                "kernel": f"gemm_pers_kernel<LNIN|BIAS|GELU> (FC1, {args.dtype}) M={M} K={K} N={N}",
                 "avg_launch_us": round(t_k * 1e6, 1)}
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

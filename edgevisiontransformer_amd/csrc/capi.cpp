@@ -721,8 +721,9 @@ int evt_graph_launch(evt_model* m, void* stream) {
 // ---- op-level entry points --------------------------------------------------------------
 
 int evt_set_gemm_variant(int variant) {
-  if (variant != 0 && variant != 1 && variant != 2 && variant != 6)
-    return fail(EVT_EINVAL, "variant must be 0, 1, 2 or 6");
+  if (variant != 0 && variant != 1 && variant != 2 && variant != 6 && variant != 8 &&
+      !(variant >= 9 && variant <= 15) && variant != 106 && variant != 108)
+    return fail(EVT_EINVAL, "variant must be 0, 1, 2, 6, 8, 9-15, 106 or 108");
   gemm_set_variant(variant);
   return EVT_OK;
 }

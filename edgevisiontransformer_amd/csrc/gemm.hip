@@ -533,12 +533,171 @@ __device__ __forceinline__ void big_epilogue(const GemmParams& p, char* smem, f3
   }
 }
 
-template <int FL, int VAR>
+
+// ---------------------------------------------------------------------------------------------
+// 8-phase ping-pong main loop (VAR 8 of gemm_big_kernel, and gemm_pers_kernel).
+// Four phases per K-tile. Each K-tile buffer is split into four 16 KiB regions: j = 0 A rows of
+// m-half 0 (of both wm), 1 W rows of n-half 0 (of all wn), 2 W n-half 1, 3 A m-half 1, read in
+// phases 1 / 1 / 2 / 3 of the tile (the wave's 128 x 64 sub-tile is done as four 64 x 32
+// quadrants, B n-half 0 stays in registers for the 4th). Region s = 4 T + j is DMA'd (2 glds
+// per lane) in global phase s - 6, i.e. into the buffer still being read, two or more phases
+// after the region's last read (WAR), and retired by a counted vmcnt before the first barrier
+// of the phase preceding its first read (RAW): every DMA gets about one K-tile of flight time
+// and 8 glds per lane stay in flight. Wave group wm = 1 runs one barrier behind group 0, so
+// while one group issues MFMAs (at raised priority) the other issues ds_reads and DMAs on the
+// same SIMD (waves w and w + 4 share a SIMD).
+// ---------------------------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void big8_bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+}
+
+// DMA region j of K-tile T into buffer T & 1.
+__device__ __forceinline__ void big8_stage(const GemmParams& p, char* smem, int wave, int lane,
+                                           int m0, int n0, int T, int j) {
+  const int srow = lane >> 3, sslot = lane & 7;
+  EVT_LDS char* base = (EVT_LDS char*)smem + (T & 1) * BIG_STAGE;
+  const int64_t koff = (int64_t)T * ROWB + ((sslot ^ srow) << 4);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (wave * 2 + i) * 8;  // region row of this wave-instruction (8 rows)
+    if (j == 0 || j == 3) {
+      const int row = (r & 63) + ((r >> 6) << 7) + (j == 3 ? 64 : 0);
+      const int gm = min(m0 + row + srow, p.M - 1);
+      glds16((const char*)p.A + (int64_t)gm * (p.lda * 2) + koff, base + row * ROWB);
+    } else {
+      const int row = ((r >> 5) << 6) + (r & 31) + (j == 2 ? 32 : 0);
+      glds16((const char*)p.W + (int64_t)(n0 + row + srow) * (p.ldw * 2) + koff,
+             base + BIG_TILE + row * ROWB);
+    }
+  }
+}
+
+__device__ __forceinline__ int big8_npro(int nk) { return min(6, 4 * nk); }
+
+__device__ __forceinline__ void big8_prologue(const GemmParams& p, char* smem, int wave, int lane,
+                                              int m0, int n0, int nk) {
+  // regions s = 0..5 (tile 0, then regions 0 / 1 of tile 1); only 0..3 when nk == 1
+#pragma unroll
+  for (int s = 0; s < 4; ++s) big8_stage(p, smem, wave, lane, m0, n0, 0, s);
+  if (nk >= 2) {
+    big8_stage(p, smem, wave, lane, m0, n0, 1, 0);
+    big8_stage(p, smem, wave, lane, m0, n0, 1, 1);
+  }
+}
+
+// One K-tile. MODE 0 steady (all DMAs, waits 8), 1 second-to-last tile, 2 last tile. X is
+// added to every wait of the tile: the number of VMEM instructions each wave is known to have
+// issued after the prologue DMAs (gemm_pers_kernel's epilogue stores; first K-tile only).
+template <int MODE, int X>
+__device__ __forceinline__ void big8_ktile(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
+                                           int wave, int lane, int wm, int wn, int m0, int n0,
+                                           int t) {
+  const int frow = lane & 15, fsw = lane & 7, fg = lane >> 4;
+  const EVT_LDS char* As = (const EVT_LDS char*)smem + (t & 1) * BIG_STAGE;
+  const EVT_LDS char* Ws = As + BIG_TILE;
+  auto rd = [&](const EVT_LDS char* S, int row, int ks) {
+    return *(const EVT_LDS u32x4*)(S + row * ROWB + (((fg + 4 * ks) ^ fsw) << 4));
+  };
+  u32x4 af[4][2], bf0[2][2], bf1[2][2];
+#pragma unroll
+  for (int ph = 0; ph < 4; ++ph) {
+    if (ph == 0) {
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) bf0[nt][ks] = rd(Ws, wn * 64 + nt * 16 + frow, ks);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) af[mt][ks] = rd(As, wm * 128 + mt * 16 + frow, ks);
+    } else if (ph == 1) {
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) bf1[nt][ks] = rd(Ws, wn * 64 + 32 + nt * 16 + frow, ks);
+    } else if (ph == 2) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) af[mt][ks] = rd(As, wm * 128 + 64 + mt * 16 + frow, ks);
+    }
+    // DMA of region s = 4 t + ph + 6
+    if (MODE == 0 || (MODE == 1 && ph < 2)) {
+      if (ph < 2) big8_stage(p, smem, wave, lane, m0, n0, t + 1, ph + 2);
+      else big8_stage(p, smem, wave, lane, m0, n0, t + 2, ph - 2);
+    }
+    // retire what the next phase reads (phases 4, 1, 2 precede reading phases)
+    if (ph != 2) {
+      if (MODE == 0) wait_vm<8 + X>();
+      else if (MODE == 1) {
+        if (ph == 3) wait_vm<4 + X>();
+        else wait_vm<8 + X>();
+      } else if (ph == 0) {
+        wait_vm<2 + X>();
+      } else if (ph == 1) {
+        wait_vm<0 + X>();
+      }
+    }
+    big8_bar();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    const int mb = (ph >= 2) ? 4 : 0, nb = (ph == 1 || ph == 2) ? 2 : 0;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          Mma<bf16>::run(nb ? bf1[nt][ks] : bf0[nt][ks], af[mt][ks], acc[nb + nt][mb + mt]);
+    __builtin_amdgcn_s_setprio(0);
+    big8_bar();
+  }
+}
+
+// Main loop over the nk K-tiles after big8_prologue (whose DMAs may be followed by X further
+// VMEM instructions per wave, or by a vmcnt(0)). Ends with every wave past a common barrier.
+template <int X>
+__device__ __forceinline__ void big8_loop(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
+                                          int wave, int lane, int wm, int wn, int m0, int n0,
+                                          int nk) {
+  if (nk >= 2) wait_vm<8 + X>();
+  else wait_vm<4 + X>();
+  big8_bar();
+  if (wm == 1) big8_bar();
+  if (nk >= 3) {
+    big8_ktile<0, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0);
+    int t = 1;
+    for (; t + 2 < nk; ++t) big8_ktile<0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t);
+    big8_ktile<1, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t);
+    big8_ktile<2, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1);
+  } else if (nk == 2) {
+    big8_ktile<1, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0);
+    big8_ktile<2, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, 1);
+  } else {
+    big8_ktile<2, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0);
+  }
+  if (wm == 0) big8_bar();
+}
+
+template <int FL, int VAR_, bool NOEPI = false>
 __global__ __launch_bounds__(512, 2) void gemm_big_kernel(GemmParams p) {
+  constexpr int VAR = VAR_;
   __shared__ __attribute__((aligned(16))) char smem[2 * BIG_STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably uniform -> SGPR math
-  const int wm = wave & 1, wn = wave >> 1;
+  // VAR 8 pairs the two waves of a SIMD across the wave groups wm = 0 / 1 (waves w, w + 4)
+  const int wm = VAR == 8 ? wave >> 2 : wave & 1, wn = VAR == 8 ? wave & 3 : wave >> 1;
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = wgid / p.ntiles, tn = wgid - tm * p.ntiles;
   const int m0 = tm * BIG_BM, n0 = tn * BIG_BN;
@@ -585,6 +744,10 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(GemmParams p) {
 #pragma unroll
       for (int mt = 0; mt < 8; ++mt) Mma<bf16>::run(w[nt], a[mt], acc[nt][mt]);
   };
+  if constexpr (VAR == 8) {
+    big8_prologue(p, smem, wave, lane, m0, n0, nk);
+    big8_loop<0>(p, smem, acc, wave, lane, wm, wn, m0, n0, nk);
+  } else {
   stage(0, 0);
   if constexpr (VAR == 6) {
     auto tile = [&](int kt, bool dma) {
@@ -630,8 +793,359 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(GemmParams p) {
       }
     }
   }
+  }
 
-  big_epilogue<FL>(p, smem, acc, wm, wn, m0, n0, tn, wave, lane);
+  if constexpr (NOEPI) {  // ablation: main loop only, accumulators kept live by a dead store
+    float sink = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sink += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (sink == 1234.5f) ((float*)p.C)[tid] = sink;
+  } else {
+    big_epilogue<FL>(p, smem, acc, wm, wn, m0, n0, tn, wave, lane);
+  }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Persistent 256x256 kernel with the epilogue in registers (bf16 output; FL without POS /
+// OUT_F32). One block per CU walks its tiles (XCD-aware: in every round an XCD takes a
+// contiguous range of logical tiles); per tile:
+//   main loop (big8_loop) -> LayerNorm coefficients / column vectors into LDS ->
+//   DMA of the NEXT tile's prologue (and its statistics / column vectors) ->
+//   epilogue of this tile straight from the accumulators, overlapping those DMAs ->
+//   the next main loop starts while this tile's output stores drain.
+// The accumulators are converted in the MFMA layout (lane: token row mt*16 + (lane & 15),
+// features 4 (lane >> 4) + j), then v_permlane16_swap pairs fragments (2k, 2k+1) so that every
+// lane holds 8 consecutive features of one row: 16-B residual loads and 16-B output stores,
+// no LDS staging of the tile. Row statistics (EPI_STATS): 64-column partials per wave, the two
+// waves of a 128-column slab combined in a fixed order (slot 2 tn + slab, as the staged
+// epilogue). Every interior tile issues its 16 output stores per wave after the next tile's
+// prologue DMAs, which is what the first K-tile's counted waits (X = 16) assume; an edge tile
+// drains with vmcnt(0) instead.
+// ---------------------------------------------------------------------------------------------
+constexpr int PERS_RAW = 2 * BIG_STAGE;         // raw LN statistics of the tile rows [256][<=8] f32x2
+constexpr int PERS_COLRAW = PERS_RAW + 16384;   // DMA'd column vectors [3][256] f32
+constexpr int PERS_COEF = PERS_COLRAW + 3072;   // LayerNorm (mu, r) per tile row [256] f32x2
+constexpr int PERS_COLB = PERS_COEF + 2048;     // column vectors of the tile being finished
+constexpr int PERS_PART = PERS_COLB + 3072;     // odd-wn waves' row partials [2][256] f32x2
+constexpr int PERS_LDS = PERS_PART + 4096;
+constexpr int PERS_X = 16;                      // output stores per wave per interior tile
+
+template <int FL>
+struct PersFlags {
+  static constexpr bool ln = (FL & (EPI_LNIN | EPI_RESLN)) != 0;
+  // column vector slots: 0 bias, 1 colsum (LNIN) or rgamma (RESLN), 2 rbeta (RESLN)
+  static constexpr bool v0 = (FL & EPI_BIAS) != 0;
+  static constexpr bool v1 = (FL & (EPI_LNIN | EPI_RESLN)) != 0;
+  static constexpr bool v2 = (FL & EPI_RESLN) != 0;
+  static_assert(!((FL & EPI_LNIN) && (FL & EPI_RESLN)), "one LayerNorm source per GEMM");
+  static_assert(!(FL & (EPI_POS | EPI_OUT_F32)), "persistent kernel: bf16 outputs, no EPI_POS");
+};
+
+// DMA the tile's LN statistics rows and column vectors into LDS (before its prologue DMAs).
+template <int FL>
+__device__ __forceinline__ void pers_coop_dma(const GemmParams& p, char* smem, int wave, int lane,
+                                              int m0, int n0) {
+  typedef PersFlags<FL> F;
+  asm volatile("" : "+v"(lane));
+  if constexpr (F::ln) {
+    const float* st = (FL & EPI_LNIN) ? p.stats_in : p.rstats;
+    const int half = p.nslots >> 1;  // 16-B chunks per row
+    const int nch = 256 * half;
+    const int64_t c0 = (int64_t)m0 * half, clast = (int64_t)p.M * half - 1;
+    for (int c = wave * 64; c < nch; c += 512)
+      glds16(st + 4 * min(c0 + c + lane, clast), (EVT_LDS char*)smem + PERS_RAW + c * 16);
+  }
+  const float* v = nullptr;
+  if (wave == 0 && F::v0) v = p.bias;
+  if (wave == 1 && (FL & EPI_LNIN)) v = p.colsum;
+  if (wave == 1 && (FL & EPI_RESLN)) v = p.rgamma;
+  if (wave == 2 && F::v2) v = p.rbeta;
+  if (v) glds16(v + min(n0 + 4 * lane, p.N - 4), (EVT_LDS char*)smem + PERS_COLRAW + wave * 1024);
+}
+
+// Per-row LayerNorm coefficients (as ln_coef) and a copy of the column vectors for the epilogue.
+template <int FL>
+__device__ __forceinline__ void pers_coef(const GemmParams& p, char* smem, int tid) {
+  typedef PersFlags<FL> F;
+  asm volatile("" : "+v"(tid));
+  if (tid < 256) {
+    if constexpr (F::ln) {
+      const EVT_LDS f32x2* st = (const EVT_LDS f32x2*)(smem + PERS_RAW) + tid * p.nslots;
+      float s1 = 0.f, s2 = 0.f;
+      for (int j = 0; j < p.nslots; ++j) {
+        const f32x2 v = st[j];
+        s1 += v[0];
+        s2 += v[1];
+      }
+      const float mu = s1 * p.inv_d;
+      const float r = rsqrtf(fmaxf(s2 * p.inv_d - mu * mu, 0.f) + p.eps);
+      ((EVT_LDS f32x2*)(smem + PERS_COEF))[tid] = f32x2{mu, r};
+    }
+    const EVT_LDS float* src = (const EVT_LDS float*)(smem + PERS_COLRAW);
+    EVT_LDS float* dst = (EVT_LDS float*)(smem + PERS_COLB);
+    if (F::v0) dst[tid] = src[tid];
+    if (F::v1) dst[256 + tid] = src[256 + tid];
+    if (F::v2) dst[512 + tid] = src[512 + tid];
+  }
+}
+
+__device__ __forceinline__ f32x4 lds4(const EVT_LDS float* p) { return *(const EVT_LDS f32x4*)p; }
+
+// v_permlane16_swap_b32 on (x, y): odd 16-lane rows of x <-> even rows of y. Written on scalars:
+// applied in place to vector elements (v[j] = swap(...)[0] in a loop) hipcc 7.2 miscompiles the
+// builtin (it reuses element 0 for every j).
+__device__ __forceinline__ float swp16(float x, float y, float& yo) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, x),
+                                                  __builtin_bit_cast(unsigned, y), false, false);
+  yo = __builtin_bit_cast(float, (unsigned)r[1]);
+  return __builtin_bit_cast(float, (unsigned)r[0]);
+}
+__device__ __forceinline__ void swap_rows16(f32x4& a, f32x4& b) {
+  float y0, y1, y2, y3;
+  const float x0 = swp16(a[0], b[0], y0), x1 = swp16(a[1], b[1], y1);
+  const float x2 = swp16(a[2], b[2], y2), x3 = swp16(a[3], b[3], y3);
+  a = f32x4{x0, x1, x2, x3};
+  b = f32x4{y0, y1, y2, y3};
+}
+
+template <int FL, int DBG = 0>
+__device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
+                                              int wave, int wm, int wn, int m0, int n0, int tn,
+                                              int lane, bool interior) {
+  asm volatile("" : "+v"(lane));  // keep lane-derived addresses out of the persistent loop (VGPRs)
+  const int frow = lane & 15, fg = lane >> 4;
+  const EVT_LDS f32x2* coef = (const EVT_LDS f32x2*)(smem + PERS_COEF);
+  const EVT_LDS float* colb = (const EVT_LDS float*)(smem + PERS_COLB);
+  // 1. MFMA layout: row wm*128 + mt*16 + frow, columns wn*64 + nt*16 + 4 fg + j
+  if constexpr ((FL & (EPI_LNIN | EPI_BIAS)) != 0) {
+    f32x4 b4[4], c4[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int c = wn * 64 + nt * 16 + 4 * fg;
+      b4[nt] = (FL & EPI_BIAS) ? lds4(colb + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if (FL & EPI_LNIN) c4[nt] = lds4(colb + 256 + c);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      float mu = 0.f, r = 0.f;
+      if (FL & EPI_LNIN) {
+        const f32x2 cf = coef[wm * 128 + mt * 16 + frow];
+        mu = cf[0];
+        r = cf[1];
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        if (FL & EPI_LNIN) acc[nt][mt] = acc[nt][mt] * r - c4[nt] * (r * mu) + b4[nt];
+        else acc[nt][mt] += b4[nt];
+      }
+    }
+  }
+  if constexpr ((FL & EPI_GELU) != 0) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[nt][mt][j] = gelu_tanh(acc[nt][mt][j]);
+  }
+  // 2. store layout: pair (2k, 2k+1) -> lane row wm*128 + (2k + (fg & 1))*16 + frow, columns
+  //    wn*64 + nt*16 + (fg >> 1)*8 + [acc[nt][2k][0..3], acc[nt][2k+1][0..3]]
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) swap_rows16(acc[nt][2 * k], acc[nt][2 * k + 1]);
+  const int rl = wm * 128 + (fg & 1) * 16 + frow;  // + 32 k
+  const int cl = wn * 64 + (fg >> 1) * 8;           // + 16 nt
+  bool rok[4], cok[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) rok[k] = interior || m0 + rl + 32 * k < p.M;
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) cok[nt] = interior || n0 + cl + 16 * nt < p.N;
+  // 3. residual (16-B loads in the store layout, all issued up front), bf16 stores and the row
+  //    statistics of the stored values; nt-major so each column-vector slice is read once
+  u32x4 rr[4][4];
+  if constexpr ((FL & EPI_RESID) != 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        rr[k][nt] = u32x4{0u, 0u, 0u, 0u};
+        if (rok[k] && cok[nt])
+          rr[k][nt] = *(const u32x4*)((const bf16*)p.resid + (int64_t)(m0 + rl + 32 * k) * p.ldr +
+                                      n0 + cl + 16 * nt);
+      }
+  }
+  f32x2 rc[4], st[4];
+  u32x4 ov[4][4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    rc[k] = (FL & EPI_RESLN) ? coef[rl + 32 * k] : f32x2{0.f, 0.f};
+    st[k] = f32x2{0.f, 0.f};
+  }
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int c = cl + 16 * nt;
+    f32x4 g[2], be[2];
+    if (FL & EPI_RESLN) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        g[h] = lds4(colb + 256 + c + 4 * h);
+        be[h] = lds4(colb + 512 + c + 4 * h);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f32x4 a = acc[nt][2 * k], b = acc[nt][2 * k + 1];
+      if constexpr ((FL & EPI_RESID) != 0) {
+        const bf16x8 r8 = __builtin_bit_cast(bf16x8, rr[k][nt]);
+        f32x4 rv[2] = {f32x4{(float)r8[0], (float)r8[1], (float)r8[2], (float)r8[3]},
+                       f32x4{(float)r8[4], (float)r8[5], (float)r8[6], (float)r8[7]}};
+        if (FL & EPI_RESLN) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) rv[h] = (rv[h] - rc[k][0]) * rc[k][1] * g[h] + be[h];
+        }
+        a += rv[0];
+        b += rv[1];
+      }
+      const bf16x8 o = {(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3],
+                        (bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
+      ov[k][nt] = __builtin_bit_cast(u32x4, o);
+      if (FL & EPI_STATS) {
+        if (cok[nt]) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float x = (float)o[e];
+            st[k][0] += x;
+            st[k][1] += x * x;
+          }
+        }
+      }
+    }
+  }
+  // 4. output: per row pair k, the wave's 32 x 64 block goes through its private 4 KiB of LDS
+  //    (free during the epilogue: buffer-1 regions 2 / 3 are only DMA'd in the next tile's
+  //    phases 1 / 2) and leaves as whole 128-B row segments, 8 rows per store instruction
+  {
+    const int w = wave;
+    EVT_LDS char* scr = (EVT_LDS char*)smem +
+                        (w < 4 ? (96 + 4 + 8 * w) * 1024 : (72 + (w - 4) * 4 + ((w - 4) >> 1) * 8) * 1024);
+    const int wrow = (fg & 1) * 16 + frow;               // store-layout row within the pair
+    const int rrow = lane >> 3, rch = lane & 7;          // row-layout lane: row i*8 + rrow, chunk
+    const bool rcol_ok = interior || n0 + wn * 64 + rch * 8 < p.N;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int ch = 2 * nt + (fg >> 1);
+        *(EVT_LDS u32x4*)(scr + wrow * 128 + ((ch ^ (wrow & 7)) << 4)) = ov[k][nt];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = i * 8 + rrow;
+        const u32x4 v = *(const EVT_LDS u32x4*)(scr + r * 128 + ((rch ^ (r & 7)) << 4));
+        const int m = m0 + wm * 128 + 32 * k + r;
+        bool keep = true;
+        if (DBG == 1) {  // ablation: no stores, every value stays live
+          keep = (v[0] ^ v[1] ^ v[2] ^ v[3]) == 0x12345u;
+        }
+        if ((interior || m < p.M) && rcol_ok && keep) {
+          u32x4* cp = (u32x4*)((bf16*)p.C + (int64_t)m * p.ldc + n0 + wn * 64 + rch * 8);
+          __builtin_nontemporal_store(v, cp);  // whole lines: streamed past L2
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  }
+  if constexpr ((FL & EPI_STATS) != 0) {
+    // lanes fg and fg ^ 2 hold the two 32-column halves of the same row
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      st[k][0] += __shfl_xor(st[k][0], 32, 64);
+      st[k][1] += __shfl_xor(st[k][1], 32, 64);
+    }
+    EVT_LDS f32x2* part = (EVT_LDS f32x2*)(smem + PERS_PART) + (wn >> 1) * 256;
+    if ((wn & 1) && lane < 32) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) part[rl + 32 * k] = st[k];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    big8_bar();
+    if (!(wn & 1) && lane < 32) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int m = m0 + rl + 32 * k;
+        const f32x2 o = part[rl + 32 * k];
+        if (interior || m < p.M)
+          *(f32x2*)(p.stats_out + 2 * ((int64_t)p.nslots * m + 2 * tn + (wn >> 1))) = st[k] + o;
+      }
+    }
+  }
+}
+
+template <int FL, int DBG = 0>
+__global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int total) {
+  __shared__ __attribute__((aligned(16))) char smem[PERS_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int G = gridDim.x;  // XCD-aware order when a multiple of 8
+  int tile = (G & 7) ? (int)blockIdx.x : (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  if (tile >= total) return;
+  const int nk = p.K / 64;
+  int tm = tile / p.ntiles, tn = tile - tm * p.ntiles;
+  if (DBG == 5) {  // experiment: stagger the blocks' start
+    const int q = (blockIdx.x >> 3) & 3;
+    for (int i = 0; i < q * nk; ++i) __builtin_amdgcn_s_sleep(20);
+  }
+  pers_coop_dma<FL>(p, smem, wave, lane, tm * BIG_BM, tn * BIG_BN);
+  big8_prologue(p, smem, wave, lane, tm * BIG_BM, tn * BIG_BN, nk);
+  wait_vmcnt0();  // the first K-tile's waits assume PERS_X younger VMEM ops or a drain
+  int iter = 0;
+  auto stamp = [&](int k) {  // DBG 3: timeline of block's tiles (s_memtime, wave 0)
+    if ((DBG == 3 || DBG == 5) && tid == 0 && iter < 16)
+      ((unsigned long long*)p.pos)[((int64_t)blockIdx.x * 16 + iter) * 4 + k] = __builtin_amdgcn_s_memtime();
+  };
+  while (true) {
+    const int m0 = tm * BIG_BM, n0 = tn * BIG_BN;
+    stamp(0);
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int ln = lane;
+    asm volatile("" : "+v"(ln));  // per-tile lane addresses: not hoisted out of the tile loop
+    big8_loop<PERS_X>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk);
+    stamp(1);
+    pers_coef<FL>(p, smem, tid);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    big8_bar();
+    const int next = tile + G;
+    const bool has_next = next < total;
+    int ntm = 0, ntn = 0;
+    if (has_next) {
+      ntm = next / p.ntiles;
+      ntn = next - ntm * p.ntiles;
+      pers_coop_dma<FL>(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN);
+      big8_prologue(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nk);
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    stamp(2);
+    const bool interior = (m0 + BIG_BM <= p.M) && (n0 + BIG_BN <= p.N);
+    pers_epilogue<FL, DBG>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior);
+    stamp(3);
+    ++iter;
+    if (!has_next) break;
+    if (!interior || DBG == 1) wait_vmcnt0();
+    tile = next;
+    tm = ntm;
+    tn = ntn;
+  }
 }
 
 template <int FL>
@@ -642,15 +1156,68 @@ hipError_t launch_big(const GemmParams& p, hipStream_t s) {
   const dim3 grid(mtiles * q.ntiles);
   if (g_gemm_variant == 2)
     hipLaunchKernelGGL((gemm_big_kernel<FL, 0>), grid, dim3(512), 0, s, q);
+  else if (g_gemm_variant == 8)
+    hipLaunchKernelGGL((gemm_big_kernel<FL, 8>), grid, dim3(512), 0, s, q);
+  else if (g_gemm_variant == 106)
+    hipLaunchKernelGGL((gemm_big_kernel<FL, 6, true>), grid, dim3(512), 0, s, q);
+  else if (g_gemm_variant == 108)
+    hipLaunchKernelGGL((gemm_big_kernel<FL, 8, true>), grid, dim3(512), 0, s, q);
   else
     hipLaunchKernelGGL((gemm_big_kernel<FL, 6>), grid, dim3(512), 0, s, q);
+  return hipGetLastError();
+}
+
+int g_num_cus = 0;
+
+constexpr bool pers_fl(int fl) {
+  return fl == 0 || fl == EPI_BIAS || fl == (EPI_BIAS | EPI_GELU) || fl == (EPI_LNIN | EPI_BIAS) ||
+         fl == (EPI_LNIN | EPI_BIAS | EPI_GELU) ||
+         fl == (EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS);
+}
+
+// persistent kernel: supported epilogue, 8-column output groups, LN rows of <= 8 slots
+bool use_pers(const GemmParams& p, int flags) {
+  if (g_gemm_variant != 0 && (g_gemm_variant < 9 || g_gemm_variant > 15 || g_gemm_variant == 12 ||
+                              g_gemm_variant == 14))
+    return false;
+  if (p.N % 8 || p.vec_ok < 2) return false;
+  if ((flags & (EPI_LNIN | EPI_RESLN)) && (p.nslots > 8 || p.nslots % 2 || p.stats_step > 1))
+    return false;
+  return true;
+}
+
+template <int FL>
+hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
+  if (!g_num_cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  GemmParams q = p;
+  q.ntiles = (p.ntiles * GEMM_BN) / BIG_BN;
+  const int total = ((p.M + BIG_BM - 1) / BIG_BM) * q.ntiles;
+  int G = min(total, g_gemm_variant == 10 ? 8 : g_num_cus);  // 10: few blocks, many tiles each
+  if (G >= 8) G &= ~7;
+  if (g_gemm_variant == 11)
+    hipLaunchKernelGGL((gemm_pers_kernel<FL, 1>), dim3(G), dim3(512), 0, s, q, total);
+  else if (g_gemm_variant == 13)  // timeline probe: p.pos = u64 [blocks][16][4]
+    hipLaunchKernelGGL((gemm_pers_kernel<FL, 3>), dim3(G), dim3(512), 0, s, q, total);
+  else if (g_gemm_variant == 15)  // timeline probe + staggered block start
+    hipLaunchKernelGGL((gemm_pers_kernel<FL, 5>), dim3(G), dim3(512), 0, s, q, total);
+  else
+    hipLaunchKernelGGL((gemm_pers_kernel<FL>), dim3(G), dim3(512), 0, s, q, total);
   return hipGetLastError();
 }
 
 template <typename T, int FL>
 hipError_t launch_t(const GemmParams& p, hipStream_t s) {
   if constexpr (std::is_same<T, bf16>::value) {
-    if (use_big(p, FL)) return launch_big<FL>(p, s);
+    if (use_big(p, FL)) {
+      if constexpr (pers_fl(FL)) {
+        if (use_pers(p, FL)) return launch_pers<FL>(p, s);
+      }
+      return launch_big<FL>(p, s);
+    }
   }
   const int mtiles = (p.M + GEMM_BM - 1) / GEMM_BM;
   hipLaunchKernelGGL((gemm_nt_kernel<T, FL>), dim3(mtiles * p.ntiles), dim3(256), 0, s, p);

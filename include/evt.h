@@ -102,9 +102,9 @@ int evt_model_destroy(evt_model* model);
 /* ---- op-level entry points (one per hot-path kernel; used by the parity tests) ---------- */
 
 /* GEMM tile-shape policy for bf16 (process-wide tuning knob): 0 = automatic (256x256 tiles when
- * the problem has >= 256 of them, else 128x128), 1 = always 128x128, 2 / 6 = 256x256 tiles with
- * the plain / interleaved main loop whenever the packed width allows (and the output rows are
- * 16-B aligned for bf16). */
+ * the problem has >= 256 of them, else 128x128), 1 = always 128x128, 2 / 6 / 8 = 256x256 tiles
+ * with the plain / interleaved / 8-phase ping-pong main loop whenever the packed width allows
+ * (and the output rows are 16-B aligned for bf16). */
 int evt_set_gemm_variant(int variant);
 
 /* Pack a Keras [K, N] fp32 kernel into the GEMM operand layout Wp[Npad][Kpad] (dtype), zero

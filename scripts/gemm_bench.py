@@ -43,6 +43,13 @@ for name, (K, N, fl) in shapes.items():
     stats[:, 0, 0], stats[:, 0, 1] = Af.sum(1), (Af * Af).sum(1)
     del Af
     colsum = torch.randn(npad, generator=g, device="cuda")
+    nso = 2 * ((N + 255) // 256)
+    rst = torch.zeros((M, nso, 2), device="cuda")
+    Rf = R.float()
+    rst[:, 0, 0], rst[:, 0, 1] = Rf.sum(1), (Rf * Rf).sum(1)
+    del Rf
+    rg, rb = torch.ones(N, device="cuda"), torch.zeros(N, device="cuda")
+    sto = torch.zeros((M, nso, 2), device="cuda")
     outs = {}
     for v in VARS:
         outs[v] = torch.empty((M, N + LDC_PAD), dtype=torch.float32 if fl & 16 else torch.bfloat16,
@@ -54,6 +61,11 @@ for name, (K, N, fl) in shapes.items():
         a.C, a.ldc, a.M, a.N, a.bias = outs[v].data_ptr(), N + LDC_PAD, M, N, bias.data_ptr()
         if fl & 4:
             a.resid, a.ldr = R.data_ptr(), N
+        if fl & 64:
+            a.rstats, a.rgamma, a.rbeta, a.ln_width = rst.data_ptr(), rg.data_ptr(), rb.data_ptr(), N
+            a.ln_eps = 1e-5
+        if fl & 128:
+            a.stats_out = sto.data_ptr()
         if fl & 32:
             a.colsum, a.stats_in, a.ln_width, a.ln_eps = colsum.data_ptr(), stats.data_ptr(), K, 1e-5
         _lib.check(lib.evt_dense(1, ctypes.byref(a), S()))

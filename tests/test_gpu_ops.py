@@ -35,7 +35,7 @@ def _gelu(x):
                                    (1000, 576, 192), (64, 64, 1000), (257, 3072, 768),
                                    (300, 128, 200)])
 @pytest.mark.parametrize("flags", [0, 3, 21, 17])
-@pytest.mark.parametrize("variant", [1, 2, 0])
+@pytest.mark.parametrize("variant", [1, 2, 8, 9, 10, 0])
 def test_dense(gpu, dtype, M, K, N, flags, variant):
     """variant 1: 128x128-tile kernel; 2: 256x256-tile kernel (bf16 only; f32 ignores it)."""
     _lib.load_library().evt_set_gemm_variant(variant)
@@ -187,9 +187,9 @@ def _stats32(xq):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f32"])
-@pytest.mark.parametrize("variant", [1, 2, 0])
+@pytest.mark.parametrize("variant", [1, 2, 8, 9, 10, 0])
 @pytest.mark.parametrize("M,D,N,gelu", [(300, 768, 2304, False), (600, 384, 1536, True),
-                                        (197, 192, 537, True)])
+                                        (197, 192, 537, True), (2900, 768, 3072, True)])
 def test_dense_layernorm_folded_input(gpu, dtype, variant, M, D, N, gelu):
     """QKV / FC1 as run in the model: A = raw stream x, LayerNorm applied per row in the epilogue
     from (sum, sumsq) statistics, gamma folded into the packed weights (gemm.hip header)."""
@@ -219,8 +219,9 @@ def test_dense_layernorm_folded_input(gpu, dtype, variant, M, D, N, gelu):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f32"])
-@pytest.mark.parametrize("variant", [1, 2, 0])
-@pytest.mark.parametrize("M,K,D", [(300, 768, 768), (513, 3072, 384), (197, 576, 192)])
+@pytest.mark.parametrize("variant", [1, 2, 8, 9, 10, 0])
+@pytest.mark.parametrize("M,K,D", [(300, 768, 768), (513, 3072, 384), (197, 576, 192),
+                                   (2900, 768, 768)])
 def test_dense_layernorm_residual_and_stats(gpu, dtype, variant, M, K, D):
     """out-proj / FC2 as run in the model: + bias + LN(resid) residual (the reference's quirk:
     the residual is the normalised input), storing the new stream and its row statistics."""
