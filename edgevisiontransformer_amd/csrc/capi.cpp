@@ -111,6 +111,7 @@ struct evt_model {
   void* o = nullptr;         // [B*T, inner]
   void* hbuf = nullptr;      // [B*T, ffn_st]
   void* hh = nullptr;        // [B, head_st]
+  void* sk = nullptr;        // stream-K scratch of the model's GEMMs (gemm_sk_bytes)
   size_t ws_bytes = 0;
   hipGraph_t graph = nullptr;        // evt_graph_capture
   hipGraphExec_t graph_exec = nullptr;
@@ -259,6 +260,7 @@ int dense(const evt_model* m, const DenseW& w, const DenseCall& c, hipStream_t s
   p.eps = 1e-5f;  // Keras LayerNormalization(epsilon=1e-5), reference norm.py:6
   p.nslots = stats_slots(width);
   p.stats_step = c.stats_step;
+  gemm_sk_bind(m->sk, p);
   EVT_HIP(gemm_launch(m->dtype, c.flags, p, s), "dense");
   return EVT_OK;
 }
@@ -289,9 +291,14 @@ int build_encoder(evt_model* m, const float* const* w, hipStream_t s) {
   return EVT_OK;
 }
 
-// Token-stream workspace of the encoder for B images (hbuf_bytes: the FFN hidden buffer).
-int alloc_encoder_ws(evt_model* m, int B, size_t hbuf_bytes) {
+// Token-stream workspace of the encoder for B images (hbuf_bytes: the FFN hidden buffer), and the
+// stream-K scratch of the model's GEMMs (its flag block zeroed once; kernels leave it zeroed).
+int alloc_encoder_ws(evt_model* m, int B, size_t hbuf_bytes, hipStream_t s) {
   const size_t es = elem_size(m->dtype);
+  if (m->dtype == DT_BF16) {
+    EVT_RC(dev_alloc(m, &m->sk, gemm_sk_bytes()));
+    EVT_HIP(hipMemsetAsync(m->sk, 0, 4096, s), "memset stream-K flags");
+  }
   const size_t rows = (size_t)B * m->sh.T;
   EVT_RC(dev_alloc(m, &m->x, rows * m->D * es));
   EVT_RC(dev_alloc(m, &m->xm, rows * m->D * es));
@@ -493,7 +500,7 @@ int evt_vit_create(const evt_vit_desc* desc, const float* const* w, int n_weight
     const int B = desc->max_batch;
     const size_t es = elem_size(desc->dtype);
     EVT_RC(alloc_encoder_ws(m, B, std::max((size_t)B * sh.T * sh.max_ffn_st,
-                                           (size_t)B * sh.P * sh.pd) * es));
+                                           (size_t)B * sh.P * sh.pd) * es, s));
     m->apatch = m->hbuf;
     EVT_RC(dev_alloc(m, &m->hh, (size_t)B * sh.head_st * es));
     m->ws_bytes = workspace_bytes(desc, sh, B);
@@ -612,7 +619,7 @@ int evt_t2t_create(const evt_t2t_desc* desc, const float* const* w, int n_weight
     EVT_RC(dev_alloc(m, &m->pout, t1 * 64 * es));
     EVT_RC(dev_alloc(m, (void**)&m->part, performer_part_floats(B, ts.grid[0] * ts.grid[0]) *
                                               sizeof(float)));
-    EVT_RC(alloc_encoder_ws(m, B, (size_t)B * ts.enc.T * ts.enc.max_ffn_st * es));
+    EVT_RC(alloc_encoder_ws(m, B, (size_t)B * ts.enc.T * ts.enc.max_ffn_st * es, s));
     m->ws_bytes = t2t_workspace_bytes(desc, ts, B);
     EVT_HIP(hipStreamSynchronize(s), "create sync");
     return EVT_OK;
@@ -722,8 +729,8 @@ int evt_graph_launch(evt_model* m, void* stream) {
 
 int evt_set_gemm_variant(int variant) {
   if (variant != 0 && variant != 1 && variant != 2 && variant != 6 && variant != 8 &&
-      !(variant >= 9 && variant <= 15) && variant != 106 && variant != 108)
-    return fail(EVT_EINVAL, "variant must be 0, 1, 2, 6, 8, 9-15, 106 or 108");
+      !(variant >= 9 && variant <= 16) && variant != 106 && variant != 108)
+    return fail(EVT_EINVAL, "variant must be 0, 1, 2, 6, 8, 9-16, 106 or 108");
   gemm_set_variant(variant);
   return EVT_OK;
 }
@@ -775,6 +782,14 @@ int evt_dense(int dtype, const evt_dense_args* a, void* stream) {
   p.eps = a->ln_eps;
   p.nslots = a->ln_width > 0 ? stats_slots(a->ln_width) : 1;
   p.stats_step = a->stats_step;
+  if (dtype == EVT_DTYPE_BF16) {  // op-level calls share one stream-K scratch (one stream at a time)
+    static void* sk = nullptr;
+    if (!sk) {
+      EVT_HIP(hipMalloc(&sk, gemm_sk_bytes()), "hipMalloc stream-K scratch");
+      EVT_HIP(hipMemset(sk, 0, 4096), "memset stream-K flags");
+    }
+    gemm_sk_bind(sk, p);
+  }
   hipError_t e = gemm_launch(dtype, f, p, (hipStream_t)stream);
   if (e == hipErrorInvalidValue) return fail(EVT_EINVAL, "dense: unsupported flags/shape");
   EVT_HIP(e, "dense");

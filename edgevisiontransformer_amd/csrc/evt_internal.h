@@ -44,6 +44,8 @@ struct GemmParams {
   float eps;                          // LayerNorm epsilon (1e-5)
   int nslots;                         // stats rows are [nslots][2]: per-128-column-slab partials
   int stats_step;                     // EPI_LNIN: A row m reads stats_in row m * stats_step (0 = 1)
+  int* sk_flags;                      // stream-K hand-off flags [>= #CUs] (zero between launches)
+  float* sk_part;                     // stream-K partial tiles [#CUs][256 * 256] fp32
 };
 constexpr int GEMM_BM = 128;
 constexpr int GEMM_BN = 128;
@@ -52,7 +54,11 @@ constexpr int PAD_K = 64;   // K granularity (elements) of every packed operand
 constexpr int PAD_N = 64;   // column granularity of activation buffers
 
 hipError_t gemm_launch(int dtype, int flags, const GemmParams& p, hipStream_t s);
-void gemm_set_variant(int v);  // 0 auto, 1 force 128x128 tiles, 2 force 256x256 (bf16)
+void gemm_set_variant(int v);
+// Bytes of the stream-K scratch of one GEMM stream (flags block first, zero it once after
+// allocating: the kernel leaves every flag at 0); gemm_sk_bind splits it into the two arrays.
+size_t gemm_sk_bytes();
+void gemm_sk_bind(void* ws, GemmParams& p);  // 0 auto, 1 force 128x128 tiles, 2 force 256x256 (bf16)
 hipError_t pack_weight(int dtype, const float* W, const float* row_scale, int K, int N, void* Wp,
                        int Kpad, int Npad, hipStream_t s);
 // colsum[n] = sum_k Wp[n][k]; cvec[n] = sum_k beta[k] W[k][n] + bias[n] (bias may be null).

@@ -1148,6 +1148,151 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Stream-K persistent kernel. The persistent kernel above runs every CU through identical tiles
+// in lock step, so all 256 epilogues (32 MB of output stores, plus 32 MB of residual loads for
+// out-proj / FC2) hit HBM in the same few microseconds while it idles during the main loops:
+// measured (scripts/probe/pers_timeline.py) 10k of a 51k-cycle FC1 tile and 25k of a 60k-cycle
+// out-proj tile are epilogue, HBM-write bound. Here the K-iterations of all tiles (total * nk)
+// are split evenly over the G blocks: block r (XCD-major rank) takes the contiguous range
+// [r I / G, (r+1) I / G). Ranges start part-way through a tile, so tile boundaries - and with
+// them the epilogue bursts - are spread uniformly over the tile period across CUs, and the tail
+// quantisation of the tile grid disappears (out-proj / FC2: 4.62 tiles per CU, not 5).
+// A tile cut by a range boundary (at most two parts: requires total >= G) is finished by
+// whichever of its two blocks gets there second:
+//   flag[b] (b = the boundary's upper rank) 0 -> 1 by CAS (first arriver), which writes its fp32
+//   partial accumulators to slot b (write-through sc1 stores, every wave drained, barrier) and
+//   sets 2; the second arriver polls for 2 (the first is running, so this always completes),
+//   resets the flag to 0 (self-cleaning: every flag is 0 again at kernel end), adds the partial
+//   (sc1 loads) and runs the normal epilogue. The LayerNorm fold / bias / residual are applied
+//   once, to the summed accumulators. Results are deterministic for a given (M, N, K, G); a split
+//   tile sums its two K ranges in a different order than an unsplit one (fp32 reassociation).
+// ---------------------------------------------------------------------------------------------
+constexpr int SK_ROLE = PERS_LDS;          // LDS word: CAS result broadcast
+constexpr int SK_LDS = PERS_LDS + 16;
+constexpr int SK_SLOT_FLOATS = 256 * 256;  // fp32 partial tile per boundary
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sk_rsrc(float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, SK_SLOT_FLOATS * 4, 0x00020000);
+}
+
+template <int FL>
+__global__ __launch_bounds__(512, 2) void gemm_sk_kernel(GemmParams p, int total) {
+  __shared__ __attribute__((aligned(16))) char smem[SK_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int G = gridDim.x;  // multiple of 8: ranks of one XCD are consecutive (shared A panels)
+  const int r = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  const int nk = p.K / 64;
+  const int64_t I = (int64_t)total * nk;
+  int64_t it = I * r / G;
+  const int64_t end = I * (r + 1) / G;
+  // work item: K-tiles [kb, ke) of tile t; operands shifted to kb
+  auto decode = [&](int64_t i, int& t, int& kb, int& ke) {
+    t = (int)(i / nk);
+    kb = (int)(i - (int64_t)t * nk);
+    ke = (int)min<int64_t>(nk, kb + (end - i));
+  };
+  auto shifted = [&](int kb) {
+    GemmParams q = p;
+    q.A = (const bf16*)p.A + kb * 64;
+    q.W = (const bf16*)p.W + kb * 64;
+    return q;
+  };
+  int t, kb, ke;
+  decode(it, t, kb, ke);
+  int tm = t / p.ntiles, tn = t - tm * p.ntiles;
+  pers_coop_dma<FL>(p, smem, wave, lane, tm * BIG_BM, tn * BIG_BN);
+  big8_prologue(shifted(kb), smem, wave, lane, tm * BIG_BM, tn * BIG_BN, ke - kb);
+  wait_vmcnt0();
+  while (true) {
+    const int m0 = tm * BIG_BM, n0 = tn * BIG_BN;
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    big8_loop<PERS_X>(shifted(kb), smem, acc, wave, ln, wm, wn, m0, n0, ke - kb);
+    pers_coef<FL>(p, smem, tid);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    big8_bar();
+    const int64_t nit = it + (ke - kb);
+    const bool has_next = nit < end;
+    int nt_ = 0, nkb = 0, nke = 0, ntm = 0, ntn = 0;
+    if (has_next) {
+      decode(nit, nt_, nkb, nke);
+      ntm = nt_ / p.ntiles;
+      ntn = nt_ - ntm * p.ntiles;
+      pers_coop_dma<FL>(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN);
+      big8_prologue(shifted(nkb), smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nke - nkb);
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const bool interior = (m0 + BIG_BM <= p.M) && (n0 + BIG_BN <= p.N);
+    const bool whole = kb == 0 && ke == nk;
+    bool finish = whole;
+    if (!whole) {
+      const int b = kb > 0 ? r : r + 1;  // boundary inside this tile
+      int* flag = p.sk_flags + b;
+      const __amdgpu_buffer_rsrc_t rs = sk_rsrc(p.sk_part + (int64_t)b * SK_SLOT_FLOATS);
+      const int off0 = (wave * 32 * 64 + lane) * 16;  // + (nt * 8 + mt) * 1024
+      if (tid == 0) {
+        int expect = 0;
+        __hip_atomic_compare_exchange_strong(flag, &expect, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        *(EVT_LDS int*)(smem + SK_ROLE) = expect;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      big8_bar();
+      finish = *(const EVT_LDS int*)(smem + SK_ROLE) != 0;
+      if (!finish) {  // first arriver: publish the partial
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int mt = 0; mt < 8; ++mt)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[nt][mt]), rs, off0,
+                                                   (nt * 8 + mt) * 1024, 16);
+        wait_vmcnt0();  // every storing wave drained
+        big8_bar();
+        if (tid == 0) __hip_atomic_store(flag, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {  // second arriver: wait for the partial and add it
+        if (tid == 0) {  // bounded (~1 s): a corrupted flag block must not hang the GPU
+          for (int i = 0; i < (1 << 23); ++i) {
+            if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 2) break;
+            __builtin_amdgcn_s_sleep(2);
+          }
+          __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        big8_bar();
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {  // 4 loads in flight: bounded register footprint
+            u32x4 v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off0, (nt * 8 + h * 4 + j) * 1024, 16);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[nt][h * 4 + j] += __builtin_bit_cast(f32x4, v[j]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+      }
+    }
+    if (finish) pers_epilogue<FL>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior);
+    if (!whole || !interior) wait_vmcnt0();
+    if (!has_next) break;
+    it = nit;
+    t = nt_;
+    kb = nkb;
+    ke = nke;
+    tm = ntm;
+    tn = ntn;
+  }
+}
+
 template <int FL>
 hipError_t launch_big(const GemmParams& p, hipStream_t s) {
   const int mtiles = (p.M + BIG_BM - 1) / BIG_BM;
@@ -1169,6 +1314,16 @@ hipError_t launch_big(const GemmParams& p, hipStream_t s) {
 
 int g_num_cus = 0;
 
+int num_cus() {
+  if (!g_num_cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  return g_num_cus;
+}
+
+
 constexpr bool pers_fl(int fl) {
   return fl == 0 || fl == EPI_BIAS || fl == (EPI_BIAS | EPI_GELU) || fl == (EPI_LNIN | EPI_BIAS) ||
          fl == (EPI_LNIN | EPI_BIAS | EPI_GELU) ||
@@ -1177,7 +1332,7 @@ constexpr bool pers_fl(int fl) {
 
 // persistent kernel: supported epilogue, 8-column output groups, LN rows of <= 8 slots
 bool use_pers(const GemmParams& p, int flags) {
-  if (g_gemm_variant != 0 && (g_gemm_variant < 9 || g_gemm_variant > 15 || g_gemm_variant == 12 ||
+  if (g_gemm_variant != 0 && (g_gemm_variant < 9 || g_gemm_variant > 16 || g_gemm_variant == 12 ||
                               g_gemm_variant == 14))
     return false;
   if (p.N % 8 || p.vec_ok < 2) return false;
@@ -1188,11 +1343,7 @@ bool use_pers(const GemmParams& p, int flags) {
 
 template <int FL>
 hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
-  if (!g_num_cus) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
-  }
+  num_cus();
   GemmParams q = p;
   q.ntiles = (p.ntiles * GEMM_BN) / BIG_BN;
   const int total = ((p.M + BIG_BM - 1) / BIG_BM) * q.ntiles;
@@ -1209,12 +1360,34 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+constexpr int SK_MAX_G = 256;
+
+int sk_grid() { return min(num_cus(), SK_MAX_G) & ~7; }
+
+// stream-K: scratch bound, auto (0) or forced (16), every range of K-iterations at least one
+// tile long (each tile has at most two parts)
+bool use_sk(const GemmParams& p) {
+  if (!p.sk_flags || !p.sk_part || g_gemm_variant != 16) return false;  // TODO auto after GPU validation
+  const int G = sk_grid();
+  const int total = ((p.M + BIG_BM - 1) / BIG_BM) * ((p.ntiles * GEMM_BN) / BIG_BN);
+  return G >= 8 && total >= G;
+}
+
+template <int FL>
+hipError_t launch_sk(const GemmParams& p, hipStream_t s) {
+  GemmParams q = p;
+  q.ntiles = (p.ntiles * GEMM_BN) / BIG_BN;
+  const int total = ((p.M + BIG_BM - 1) / BIG_BM) * q.ntiles;
+  hipLaunchKernelGGL((gemm_sk_kernel<FL>), dim3(sk_grid()), dim3(512), 0, s, q, total);
+  return hipGetLastError();
+}
+
 template <typename T, int FL>
 hipError_t launch_t(const GemmParams& p, hipStream_t s) {
   if constexpr (std::is_same<T, bf16>::value) {
     if (use_big(p, FL)) {
       if constexpr (pers_fl(FL)) {
-        if (use_pers(p, FL)) return launch_pers<FL>(p, s);
+        if (use_pers(p, FL)) return use_sk(p) ? launch_sk<FL>(p, s) : launch_pers<FL>(p, s);
       }
       return launch_big<FL>(p, s);
     }
@@ -1291,6 +1464,13 @@ __global__ void fold_kernel(const T* __restrict__ Wp, int Kpad, const float* __r
 }  // namespace
 
 void gemm_set_variant(int v) { g_gemm_variant = v; }
+
+size_t gemm_sk_bytes() { return 4096 + (size_t)SK_MAX_G * SK_SLOT_FLOATS * sizeof(float); }
+
+void gemm_sk_bind(void* ws, GemmParams& p) {
+  p.sk_flags = ws ? (int*)ws : nullptr;
+  p.sk_part = ws ? (float*)((char*)ws + 4096) : nullptr;
+}
 
 hipError_t gemm_launch(int dtype, int flags, const GemmParams& p, hipStream_t s) {
   if (p.M <= 0 || p.N <= 0) return hipSuccess;

@@ -102,9 +102,12 @@ int evt_model_destroy(evt_model* model);
 /* ---- op-level entry points (one per hot-path kernel; used by the parity tests) ---------- */
 
 /* GEMM tile-shape policy for bf16 (process-wide tuning knob): 0 = automatic (256x256 tiles when
- * the problem has >= 256 of them, else 128x128), 1 = always 128x128, 2 / 6 / 8 = 256x256 tiles
- * with the plain / interleaved / 8-phase ping-pong main loop whenever the packed width allows
- * (and the output rows are 16-B aligned for bf16). */
+ * the problem has >= 256 of them, else 128x128; among 256x256 GEMMs with a fused epilogue the
+ * stream-K persistent kernel when there are at least #CUs tiles, else the tile-persistent one),
+ * 1 = always 128x128, 2 / 6 / 8 = 256x256 tiles with the plain / interleaved / 8-phase ping-pong
+ * main loop whenever the packed width allows (and the output rows are 16-B aligned for bf16),
+ * 9 = tile-persistent kernel (no stream-K), 16 = stream-K where it applies; 10-15 and 106 / 108
+ * are diagnostic builds (timeline stamps, main loop only). */
 int evt_set_gemm_variant(int variant);
 
 /* Pack a Keras [K, N] fp32 kernel into the GEMM operand layout Wp[Npad][Kpad] (dtype), zero
