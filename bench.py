@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=512, help="images per GPU")
     ap.add_argument("--model", default="deit_base",
                     choices=["deit_base", "deit_small", "deit_tiny", "t2t_vit_7", "t2t_vit_10",
-                             "t2t_vit_12", "t2t_vit_14"])
+                             "t2t_vit_12", "t2t_vit_14", "swin_tiny", "swin_small", "swin_base"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-probe", action="store_true", help="skip the per-kernel probe")
@@ -102,7 +102,14 @@ def kernel_probe(dtype: str, M: int, K: int, N: int, iters: int = 20) -> float:
 
 def cpu_baseline(model_name: str, budget_s: float) -> dict:
     from edgevisiontransformer_amd.weights import make_images, make_t2t_params, make_vit_params
-    if model_name.startswith("t2t"):
+    if model_name.startswith("swin"):
+        from oracle.swin_ref import swin_forward as fwd
+        from edgevisiontransformer_amd.modeling.models.swin import swin_config_from_name
+        from edgevisiontransformer_amd.weights import make_swin_params
+        cfg = swin_config_from_name(f"{model_name}_patch4_window7_224")
+        params = make_swin_params(cfg, seed=0)
+        layout, src = "NCHW", "oracle/swin_ref.py"
+    elif model_name.startswith("t2t"):
         from oracle.t2t_ref import t2t_vit_forward as fwd
         from edgevisiontransformer_amd.modeling.models.t2t_vit import t2t_cfg_for
         cfg = t2t_cfg_for(model_name)
@@ -171,7 +178,10 @@ def main():
                           "N": cfg.ffn[0]}), flush=True)
         return
     t2t = args.model.startswith("t2t")
-    if t2t:
+    swin = args.model.startswith("swin")
+    if swin:
+        from edgevisiontransformer_amd.modeling.models import swin as mod
+    elif t2t:
         from edgevisiontransformer_amd.modeling.models import t2t_vit as mod
     else:
         from edgevisiontransformer_amd.modeling.models import vit as mod
@@ -211,7 +221,7 @@ def main():
     imgs_per_s = world * B * args.steps / el
     peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
     roof = None
-    if rank == 0 and not args.no_probe:
+    if rank == 0 and not args.no_probe and not swin:
         ffn = model.cfg.mlp_dim if t2t else model.cfg.ffn[0]
         M, K, N = B * model.cfg.tokens, model.cfg.dim, ffn
         t_k = kernel_probe(args.dtype, M, K, N)
@@ -231,10 +241,11 @@ def main():
             "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic N(0,1) NCHW images resident in HBM; deterministic random-init weights",
-            "config": {"workload": f"{args.model}/{'224' if t2t else '16-224'} forward, bs={B} per "
+            "config": {"workload": f"{args.model}/{'224' if t2t or swin else '16-224'} forward, bs={B} per "
                                    f"GPU, {args.dtype}",
                        "model": args.model, "global_batch": world * B, "per_gpu_batch": B,
-                       "seq_len": model.cfg.tokens, "parallelism": f"dp{world} (batch shard, "
+                       "seq_len": model.cfg.res(0) ** 2 if swin else model.cfg.tokens,
+                       "parallelism": f"dp{world} (batch shard, "
                        "RCCL all-gather of logits)" if world > 1 else "dp1"},
             "model_roofline": {"achieved_tflops": round(imgs_per_s * gflop_img / world / 1e3, 2),
                                "peak": peak, "frac": round(imgs_per_s * gflop_img / world / 1e3

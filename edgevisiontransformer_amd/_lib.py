@@ -25,7 +25,8 @@ DTYPE = {"f32": 0, "fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1}
 
 # GEMM epilogue flags (include/evt.h EVT_EPI_*)
 EPI_BIAS, EPI_GELU, EPI_RESID, EPI_POS, EPI_OUT_F32 = 1, 2, 4, 8, 16
-EPI_LNIN, EPI_RESLN, EPI_STATS = 32, 64, 128
+EPI_LNIN, EPI_RESLN, EPI_STATS, EPI_GELU_ERF = 32, 64, 128, 256
+SWIN_MAX_STAGES = 8
 
 
 class EvtError(RuntimeError):
@@ -65,6 +66,16 @@ class evt_t2t_desc(ctypes.Structure):
                 ("dtype", ctypes.c_int32), ("max_batch", ctypes.c_int32)]
 
 
+class evt_swin_desc(ctypes.Structure):
+    _fields_ = [("image_size", ctypes.c_int32), ("patch_size", ctypes.c_int32),
+                ("in_chans", ctypes.c_int32), ("num_classes", ctypes.c_int32),
+                ("embed_dim", ctypes.c_int32), ("num_stages", ctypes.c_int32),
+                ("depths", ctypes.c_int32 * SWIN_MAX_STAGES),
+                ("num_heads", ctypes.c_int32 * SWIN_MAX_STAGES),
+                ("window_size", ctypes.c_int32), ("mlp_ratio", ctypes.c_float),
+                ("dtype", ctypes.c_int32), ("max_batch", ctypes.c_int32)]
+
+
 # name -> (restype, argtypes); this is the full symbol list of include/evt.h
 _P, _I, _I64, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
 SIGNATURES = {
@@ -95,6 +106,14 @@ SIGNATURES = {
     "evt_performer": (_I, [_I, _P, _I64, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                            _I64, _P]),
     "evt_performer_scratch": (_I64, [_I, _I]),
+    "evt_swin_num_weights": (_I, [ctypes.POINTER(evt_swin_desc)]),
+    "evt_swin_create": (_I, [ctypes.POINTER(evt_swin_desc), ctypes.POINTER(_P), _I, _P,
+                             ctypes.POINTER(_P)]),
+    "evt_swin_forward": (_I, [_P, _P, _I, _P, _P]),
+    "evt_swin_query_workspace": (_I, [ctypes.POINTER(evt_swin_desc), _I,
+                                      ctypes.POINTER(ctypes.c_size_t)]),
+    "evt_window_attention": (_I, [_I, _P, _I64, _P, _I64, _P, _I, _I, _I, _I, _I, _P]),
+    "evt_patch_merge": (_I, [_I, _P, _I64, _I, _I, _I, _P, _P, _I, _P]),
 }
 
 _lib = None

@@ -81,6 +81,18 @@ struct Performer {  // one TokenPerformer (transformer_encoder.py:39-101)
   PerformerWeights w{};      // fp32 device copies (Keras layouts)
 };
 
+struct SwinBlock {  // one Swin block (microsoft SwinTransformerBlock)
+  int shift = 0;
+  float* bias = nullptr;     // [H][49][64] dense relative position bias (* log2 e)
+  DenseW qkv, proj, fc1, fc2;
+};
+
+struct SwinStage {
+  int C = 0, Cst = 0, H = 0, R = 0, mlp = 0, mst = 0;
+  DenseW merge;              // LN(4C)-folded reduction Linear(4C, 2C, bias=False) (stage > 0)
+  std::vector<SwinBlock> blocks;
+};
+
 struct evt_model {
   int family = 0;            // 0: ViT / ViT_Pruned, 1: T2T-ViT
   int dtype = 0, D = 0, max_batch = 0, num_classes = 0;
@@ -112,6 +124,11 @@ struct evt_model {
   void* hbuf = nullptr;      // [B*T, ffn_st]
   void* hh = nullptr;        // [B, head_st]
   void* sk = nullptr;        // stream-K scratch of the model's GEMMs (gemm_sk_bytes)
+  // Swin (family 2)
+  evt_swin_desc sdesc{};
+  std::vector<SwinStage> stages;
+  float *pnorm_g = nullptr, *pnorm_b = nullptr, *norm_g = nullptr, *norm_b = nullptr;
+  void* pooled = nullptr;    // [B, Cst_last] LayerNorm + token mean (head A operand)
   size_t ws_bytes = 0;
   hipGraph_t graph = nullptr;        // evt_graph_capture
   hipGraphExec_t graph_exec = nullptr;
@@ -225,6 +242,7 @@ struct DenseCall {
   float* stats_out = nullptr;
   int ln_width = 0;    // LayerNorm width of stats_in / rstats / stats_out (0: the model width D)
   int stats_step = 1;  // EPI_LNIN: A row m reads stats_in row m * stats_step
+  int slot_width = 0;  // width whose stats_slots() numbers the slots (0: ln_width)
 };
 
 int dense(const evt_model* m, const DenseW& w, const DenseCall& c, hipStream_t s) {
@@ -258,7 +276,7 @@ int dense(const evt_model* m, const DenseW& w, const DenseCall& c, hipStream_t s
   const int width = c.ln_width ? c.ln_width : m->D;
   p.inv_d = 1.0f / (float)width;
   p.eps = 1e-5f;  // Keras LayerNormalization(epsilon=1e-5), reference norm.py:6
-  p.nslots = stats_slots(width);
+  p.nslots = stats_slots(c.slot_width ? c.slot_width : width);
   p.stats_step = c.stats_step;
   gemm_sk_bind(m->sk, p);
   EVT_HIP(gemm_launch(m->dtype, c.flags, p, s), "dense");
@@ -420,6 +438,79 @@ size_t t2t_workspace_bytes(const evt_t2t_desc* d, const T2TShape& ts, int B) {
          performer_part_floats(B, ts.grid[0] * ts.grid[0]) * 4 + 2 * rows * d->dim * es +
          2 * rows * stats_slots(d->dim) * 2 * 4 + rows * 4 * ts.enc.max_inner * es +
          rows * ts.enc.max_ffn_st * es;
+}
+
+
+// ---- Swin geometry ------------------------------------------------------------------------
+struct SwinGeo {
+  int ns = 0;
+  int C[EVT_SWIN_MAX_STAGES], Cst[EVT_SWIN_MAX_STAGES], R[EVT_SWIN_MAX_STAGES];
+  int mlp[EVT_SWIN_MAX_STAGES], mst[EVT_SWIN_MAX_STAGES];
+  int pd = 0, pdst = 0;  // patch vector width (c, kh, kw) and its K padding
+};
+
+int validate_swin(const evt_swin_desc* d, SwinGeo* g) {
+  if (!d) return fail(EVT_EINVAL, "desc is NULL");
+  if (d->dtype != EVT_DTYPE_F32 && d->dtype != EVT_DTYPE_BF16)
+    return fail(EVT_EINVAL, "dtype must be EVT_DTYPE_F32 or EVT_DTYPE_BF16");
+  if (d->num_stages < 1 || d->num_stages > EVT_SWIN_MAX_STAGES)
+    return fail(EVT_EINVAL, "num_stages must be in [1, 8]");
+  if (d->patch_size <= 0 || d->image_size <= 0 || d->image_size % d->patch_size)
+    return fail(EVT_EINVAL, "image_size must be a multiple of patch_size");
+  if (d->in_chans <= 0 || d->num_classes <= 0 || d->max_batch <= 0 || !(d->mlp_ratio > 0.f))
+    return fail(EVT_EINVAL, "in_chans, num_classes, max_batch, mlp_ratio must be positive");
+  if (d->window_size != 7) return fail(EVT_EINVAL, "window_size must be 7 in this build");
+  if (d->embed_dim <= 0 || d->embed_dim % 32)
+    return fail(EVT_EINVAL, "embed_dim must be a positive multiple of 32");
+  g->ns = d->num_stages;
+  g->pd = d->in_chans * d->patch_size * d->patch_size;
+  g->pdst = (int)round_up(g->pd, PAD_K);
+  int R = d->image_size / d->patch_size;
+  for (int i = 0; i < g->ns; ++i) {
+    if (i > 0) {
+      if (R % 2) return fail(EVT_EINVAL, "patch merging needs an even resolution");
+      R /= 2;
+    }
+    if (R % 7) return fail(EVT_EINVAL, "every stage resolution must be a multiple of the window (7)");
+    const int C = d->embed_dim << i;
+    if (C > 1024) return fail(EVT_EINVAL, "stage width must be <= 1024");
+    if (d->depths[i] < 0) return fail(EVT_EINVAL, "depths must be >= 0");
+    if (d->num_heads[i] <= 0 || C % d->num_heads[i] || C / d->num_heads[i] != 32)
+      return fail(EVT_EINVAL, "head size (stage width / num_heads) must be 32 in this build");
+    g->C[i] = C;
+    g->Cst[i] = (int)round_up(C, PAD_N);
+    g->R[i] = R;
+    g->mlp[i] = (int)(C * d->mlp_ratio);
+    if (g->mlp[i] <= 0) return fail(EVT_EINVAL, "mlp width must be positive");
+    g->mst[i] = (int)round_up(g->mlp[i], PAD_N);
+  }
+  return EVT_OK;
+}
+
+struct SwinWs {  // element / float counts of the Swin workspace for B images
+  size_t stream = 0, stats = 0, qkv = 0, o = 0, hbuf = 0, pooled = 0;
+};
+
+SwinWs swin_ws(const SwinGeo& g, int B) {
+  SwinWs w;
+  for (int i = 0; i < g.ns; ++i) {
+    const size_t rows = (size_t)B * g.R[i] * g.R[i];
+    w.stream = std::max(w.stream, rows * g.Cst[i]);
+    w.stats = std::max(w.stats, rows * stats_slots(g.C[i]) * 2);
+    w.qkv = std::max(w.qkv, rows * 3 * g.C[i]);
+    w.o = std::max(w.o, rows * g.Cst[i]);
+    w.hbuf = std::max(w.hbuf, rows * g.mst[i]);
+    if (i > 0) w.hbuf = std::max(w.hbuf, rows * 4 * g.C[i - 1]);
+  }
+  w.hbuf = std::max(w.hbuf, (size_t)B * g.R[0] * g.R[0] * g.pdst);
+  w.pooled = (size_t)B * g.Cst[g.ns - 1];
+  return w;
+}
+
+size_t swin_workspace_bytes(const evt_swin_desc* d, const SwinGeo& g, int B) {
+  const SwinWs w = swin_ws(g, B);
+  const size_t es = elem_size(d->dtype);
+  return (2 * w.stream + w.qkv + w.o + w.hbuf + w.pooled) * es + 2 * w.stats * sizeof(float);
 }
 
 }  // namespace
@@ -699,8 +790,9 @@ int evt_graph_capture(evt_model* m, const float* img, int batch, float* logits, 
     m->graph = nullptr;
   }
   EVT_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal), "begin capture");
-  const int rc = m->family == 0 ? evt_vit_forward(m, img, batch, logits, stream)
-                                : evt_t2t_forward(m, img, batch, logits, stream);
+  const int rc = m->family == 0   ? evt_vit_forward(m, img, batch, logits, stream)
+                 : m->family == 1 ? evt_t2t_forward(m, img, batch, logits, stream)
+                                  : evt_swin_forward(m, img, batch, logits, stream);
   hipGraph_t g = nullptr;
   const hipError_t e = hipStreamEndCapture(s, &g);
   if (rc) {
@@ -722,6 +814,218 @@ int evt_graph_capture(evt_model* m, const float* img, int batch, float* logits, 
 int evt_graph_launch(evt_model* m, void* stream) {
   if (!m || !m->graph_exec) return fail(EVT_EINVAL, "no captured graph (call evt_graph_capture)");
   EVT_HIP(hipGraphLaunch(m->graph_exec, (hipStream_t)stream), "graph launch");
+  return EVT_OK;
+}
+
+// ---- Swin Transformer -------------------------------------------------------------------
+
+int evt_swin_num_weights(const evt_swin_desc* desc) {
+  if (!desc || desc->num_stages < 1 || desc->num_stages > EVT_SWIN_MAX_STAGES)
+    return fail(EVT_EINVAL, "bad desc");
+  int n = 4 + 4;
+  for (int i = 0; i < desc->num_stages; ++i) n += (i > 0 ? 3 : 0) + 13 * desc->depths[i];
+  return n;
+}
+
+int evt_swin_query_workspace(const evt_swin_desc* desc, int batch, size_t* bytes) {
+  SwinGeo g;
+  EVT_RC(validate_swin(desc, &g));
+  if (!bytes || batch <= 0) return fail(EVT_EINVAL, "bytes must be non-null and batch positive");
+  *bytes = swin_workspace_bytes(desc, g, batch);
+  return EVT_OK;
+}
+
+int evt_swin_create(const evt_swin_desc* desc, const float* const* w, int n_weights, void* stream,
+                    evt_model** out) {
+  if (!out) return fail(EVT_EINVAL, "out is NULL");
+  *out = nullptr;
+  SwinGeo g;
+  EVT_RC(validate_swin(desc, &g));
+  if (n_weights != evt_swin_num_weights(desc) || !w)
+    return fail(EVT_EINVAL, "expected " + std::to_string(evt_swin_num_weights(desc)) + " weights");
+  for (int i = 0; i < n_weights; ++i)
+    if (!w[i]) return fail(EVT_EINVAL, "weight pointer " + std::to_string(i) + " is NULL");
+  hipStream_t s = (hipStream_t)stream;
+  evt_model* m = new evt_model();
+  m->family = 2;
+  m->dtype = desc->dtype;
+  m->D = desc->embed_dim;
+  m->max_batch = desc->max_batch;
+  m->num_classes = desc->num_classes;
+  m->sdesc = *desc;
+  auto run = [&]() -> int {
+    const int E = desc->embed_dim;
+    int k = 0;
+    EVT_RC(make_dense(m, &m->patch, w[0], w[1], g.pd, E, s));  // Conv2d(k = s = patch)
+    EVT_RC(copy_vec(m, &m->pnorm_g, w[2], E, s));
+    EVT_RC(copy_vec(m, &m->pnorm_b, w[3], E, s));
+    k = 4;
+    m->stages.resize(g.ns);
+    for (int i = 0; i < g.ns; ++i) {
+      SwinStage& st = m->stages[i];
+      st.C = g.C[i];
+      st.Cst = g.Cst[i];
+      st.H = desc->num_heads[i];
+      st.R = g.R[i];
+      st.mlp = g.mlp[i];
+      st.mst = g.mst[i];
+      if (i > 0) {  // PatchMerging: LayerNorm(4C) folded into reduction Linear(4C, 2C, bias=False)
+        EVT_RC(make_dense(m, &st.merge, w[k + 2], nullptr, 4 * g.C[i - 1], st.C, s, w[k], w[k + 1]));
+        k += 3;
+      }
+      st.blocks.resize(desc->depths[i]);
+      for (int j = 0; j < desc->depths[i]; ++j) {
+        SwinBlock& bl = st.blocks[j];
+        bl.shift = (j % 2 == 1 && st.R > 7) ? 3 : 0;  // SW-MSA on odd blocks; none at R == window
+        const int C = st.C;
+        EVT_RC(make_dense(m, &bl.qkv, w[k + 2], w[k + 3], C, 3 * C, s, w[k + 0], w[k + 1]));
+        EVT_RC(dev_alloc(m, (void**)&bl.bias, (size_t)st.H * 49 * 64 * sizeof(float)));
+        EVT_HIP(rpb_dense_launch(w[k + 4], st.H, 7, bl.bias, s), "relative position bias");
+        EVT_RC(make_dense(m, &bl.proj, w[k + 5], w[k + 6], C, C, s));
+        EVT_RC(make_dense(m, &bl.fc1, w[k + 9], w[k + 10], C, st.mlp, s, w[k + 7], w[k + 8]));
+        EVT_RC(make_dense(m, &bl.fc2, w[k + 11], w[k + 12], st.mlp, C, s));
+        k += 13;
+      }
+    }
+    const int nf = g.C[g.ns - 1];
+    EVT_RC(copy_vec(m, &m->norm_g, w[k + 0], nf, s));
+    EVT_RC(copy_vec(m, &m->norm_b, w[k + 1], nf, s));
+    EVT_RC(make_dense(m, &m->head, w[k + 2], w[k + 3], nf, desc->num_classes, s));
+    const int B = desc->max_batch;
+    const SwinWs ws = swin_ws(g, B);
+    const size_t es = elem_size(desc->dtype);
+    EVT_RC(dev_alloc(m, &m->x, ws.stream * es));
+    EVT_RC(dev_alloc(m, &m->xm, ws.stream * es));
+    EVT_RC(dev_alloc(m, (void**)&m->sx, ws.stats * sizeof(float)));
+    EVT_RC(dev_alloc(m, (void**)&m->sm, ws.stats * sizeof(float)));
+    EVT_RC(dev_alloc(m, &m->qkv, ws.qkv * es));
+    EVT_RC(dev_alloc(m, &m->o, ws.o * es));
+    EVT_RC(dev_alloc(m, &m->hbuf, ws.hbuf * es));
+    EVT_RC(dev_alloc(m, &m->pooled, ws.pooled * es));
+    if (desc->dtype == DT_BF16) {
+      EVT_RC(dev_alloc(m, &m->sk, gemm_sk_bytes()));
+      EVT_HIP(hipMemsetAsync(m->sk, 0, 4096, s), "memset stream-K flags");
+    }
+    m->ws_bytes = swin_workspace_bytes(desc, g, B);
+    EVT_HIP(hipStreamSynchronize(s), "create sync");
+    return EVT_OK;
+  };
+  return finish_create(m, run(), out);
+}
+
+int evt_swin_forward(evt_model* m, const float* img, int B, float* logits, void* stream) {
+  if (!m || !img || !logits) return fail(EVT_EINVAL, "model, img and logits must be non-null");
+  if (m->family != 2) return fail(EVT_EINVAL, "model is not a Swin Transformer");
+  if (B <= 0 || B > m->max_batch)
+    return fail(EVT_EINVAL, "batch must be in [1, max_batch=" + std::to_string(m->max_batch) + "]");
+  hipStream_t s = (hipStream_t)stream;
+  const evt_swin_desc& d = m->sdesc;
+  const int dt = d.dtype;
+  const SwinStage& s0 = m->stages[0];
+  const int pdst = (int)round_up(d.in_chans * d.patch_size * d.patch_size, PAD_K);
+  const float scale_log2 = 0.17677669529663687f * 1.4426950408889634f;  // 32^-0.5 * log2(e)
+  // patch embed: Conv2d(k = s = patch) as im2col + Dense, then its LayerNorm -> stream x + stats
+  int rows = B * s0.R * s0.R;
+  EVT_HIP(swin_patch_launch(dt, img, B, d.in_chans, d.image_size, d.patch_size, m->hbuf, pdst, s),
+          "patch im2col");
+  {
+    DenseCall c;
+    c.flags = EPI_BIAS;
+    c.A = m->hbuf; c.lda = pdst; c.C = m->xm; c.ldc = s0.Cst; c.M = rows; c.N = s0.Cst;
+    EVT_RC(dense(m, m->patch, c, s));
+  }
+  EVT_HIP(ln_rows_launch(dt, m->xm, s0.Cst, m->x, m->pnorm_g, m->pnorm_b, rows, s0.C, 1e-5f, m->sx,
+                         stats_slots(s0.C), s),
+          "patch norm");
+  for (size_t i = 0; i < m->stages.size(); ++i) {
+    const SwinStage& st = m->stages[i];
+    const int C = st.C, Cst = st.Cst;
+    rows = B * st.R * st.R;
+    if (i > 0) {  // PatchMerging: gather -> LN(4C)-folded reduction -> stream x (+ stats)
+      const SwinStage& pv = m->stages[i - 1];
+      EVT_HIP(merge_launch(dt, m->x, pv.Cst, B, pv.R, pv.C, m->hbuf, m->sm, stats_slots(C), s),
+              "patch merge");
+      DenseCall c;
+      c.flags = EPI_LNIN | EPI_BIAS | EPI_STATS;
+      c.A = m->hbuf; c.lda = 4 * pv.C; c.C = m->x; c.ldc = Cst; c.M = rows; c.N = Cst;
+      c.stats_in = m->sm; c.stats_out = m->sx; c.ln_width = 4 * pv.C; c.slot_width = C;
+      EVT_RC(dense(m, st.merge, c, s));
+    }
+    for (const SwinBlock& bl : st.blocks) {
+      {  // LN1-folded QKV (+ bias)
+        DenseCall c;
+        c.flags = EPI_LNIN | EPI_BIAS;
+        c.A = m->x; c.lda = Cst; c.C = m->qkv; c.ldc = 3 * C; c.M = rows; c.N = 3 * C;
+        c.stats_in = m->sx; c.ln_width = C;
+        EVT_RC(dense(m, bl.qkv, c, s));
+      }
+      SwinAttnParams ap{m->qkv, 3 * C, m->o, Cst, bl.bias, B, st.R, st.R / 7, C, st.H, bl.shift,
+                        scale_log2};
+      EVT_HIP(window_attn_launch(dt, ap, s), "window attention");
+      {  // proj + bias + residual x -> xm (+ stats)
+        DenseCall c;
+        c.flags = EPI_BIAS | EPI_RESID | EPI_STATS;
+        c.A = m->o; c.lda = Cst; c.C = m->xm; c.ldc = Cst; c.M = rows; c.N = Cst;
+        c.resid = m->x; c.ldr = Cst; c.stats_out = m->sm; c.ln_width = C;
+        EVT_RC(dense(m, bl.proj, c, s));
+      }
+      {  // LN2-folded FC1 + erf GELU
+        DenseCall c;
+        c.flags = EPI_LNIN | EPI_BIAS | EPI_GELU_ERF;
+        c.A = m->xm; c.lda = Cst; c.C = m->hbuf; c.ldc = st.mst; c.M = rows; c.N = st.mst;
+        c.stats_in = m->sm; c.ln_width = C;
+        EVT_RC(dense(m, bl.fc1, c, s));
+      }
+      {  // FC2 + bias + residual xm -> x (+ stats)
+        DenseCall c;
+        c.flags = EPI_BIAS | EPI_RESID | EPI_STATS;
+        c.A = m->hbuf; c.lda = st.mst; c.C = m->x; c.ldc = Cst; c.M = rows; c.N = Cst;
+        c.resid = m->xm; c.ldr = Cst; c.stats_out = m->sx; c.ln_width = C;
+        EVT_RC(dense(m, bl.fc2, c, s));
+      }
+    }
+  }
+  // final LayerNorm + mean over tokens -> head Dense (fp32 logits)
+  const SwinStage& sl = m->stages.back();
+  EVT_HIP(ln_pool_launch(dt, m->x, sl.Cst, B, sl.R * sl.R, sl.C, m->sx, stats_slots(sl.C),
+                         m->norm_g, m->norm_b, m->pooled, sl.Cst, s),
+          "norm + avgpool");
+  {
+    DenseCall c;
+    c.flags = EPI_BIAS | EPI_OUT_F32;
+    c.A = m->pooled; c.lda = sl.Cst; c.C = logits; c.ldc = d.num_classes; c.M = B;
+    c.N = d.num_classes;
+    EVT_RC(dense(m, m->head, c, s));
+  }
+  return EVT_OK;
+}
+
+int evt_window_attention(int dtype, const void* qkv, int64_t ldq, void* out, int64_t ldo,
+                         const float* rpb, int B, int R, int C, int H, int shift, void* stream) {
+  if (!qkv || !out || !rpb) return fail(EVT_EINVAL, "null pointer");
+  if (dtype != EVT_DTYPE_F32 && dtype != EVT_DTYPE_BF16) return fail(EVT_EINVAL, "bad dtype");
+  if (B < 0 || R <= 0 || R % 7 || H <= 0 || C != 32 * H || ldo < C || ldq < 3 * C || shift < 0 ||
+      shift >= 7 || ldq % 8 || ldo % 4)
+    return fail(EVT_EINVAL, "bad window-attention shape (R % 7 == 0, head size 32, 0 <= shift < 7)");
+  hipStream_t s = (hipStream_t)stream;
+  float* dense_bias = nullptr;
+  EVT_HIP(hipMallocAsync((void**)&dense_bias, (size_t)H * 49 * 64 * sizeof(float), s), "malloc bias");
+  EVT_HIP(rpb_dense_launch(rpb, H, 7, dense_bias, s), "relative position bias");
+  SwinAttnParams ap{qkv, ldq, out, ldo, dense_bias, B, R, R / 7, C, H, shift,
+                    0.17677669529663687f * 1.4426950408889634f};
+  const hipError_t e = window_attn_launch(dtype, ap, s);
+  (void)hipFreeAsync(dense_bias, s);
+  EVT_HIP(e, "window attention");
+  return EVT_OK;
+}
+
+int evt_patch_merge(int dtype, const void* x, int64_t ldx, int B, int R, int C, void* out,
+                    float* stats, int nslots, void* stream) {
+  if (!x || !out || !stats) return fail(EVT_EINVAL, "null pointer");
+  if (dtype != EVT_DTYPE_F32 && dtype != EVT_DTYPE_BF16) return fail(EVT_EINVAL, "bad dtype");
+  if (B < 0 || R <= 0 || R % 2 || C <= 0 || ldx < C || nslots <= 0 || nslots > 64)
+    return fail(EVT_EINVAL, "bad patch-merge shape");
+  EVT_HIP(merge_launch(dtype, x, ldx, B, R, C, out, stats, nslots, (hipStream_t)stream), "merge");
   return EVT_OK;
 }
 

@@ -55,6 +55,9 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
+// Exact GELU (torch nn.GELU(), the Swin MLP activation): 0.5 x (1 + erf(x / sqrt 2)).
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.7071067811865476f)); }
+
 // Wave64 reductions (butterfly over all 64 lanes).
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

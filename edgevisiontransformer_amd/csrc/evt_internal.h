@@ -18,6 +18,7 @@ enum : int {
   EPI_LNIN = 32,     // A rows are un-normalised: v = r*acc - r*mu*colsum[n] (+ bias = c[n])
   EPI_RESLN = 64,    // residual is LN(resid): (resid - mu_r) * r_r * rgamma[n] + rbeta[n]
   EPI_STATS = 128,   // accumulate (sum, sum of squares) of each output row into stats_out
+  EPI_GELU_ERF = 256,  // exact erf GELU (nn.GELU, the Swin MLP)
 };
 
 // C[M, N] = epilogue(A[M, K] . W[K, N]) with W pre-packed K-contiguous as Wp[Npad][Kpad].
@@ -115,5 +116,27 @@ hipError_t performer_launch(int dtype, const void* kqv, int64_t ldq, int B, int 
 // CLS rows x[b*ntok] = cls + pos[0] (dtype) and their LayerNorm slot statistics.
 hipError_t cls_rows_launch(int dtype, void* x, int B, int ntok, int D, const float* cls,
                            const float* pos, float* stats, hipStream_t s);
+
+// ---- Swin Transformer (swin.hip) ----
+struct SwinAttnParams {
+  const void* qkv; int64_t ldq;   // raster-order token rows [B*R*R], columns (qkv h d), head 32
+  void* out;       int64_t ldo;   // raster-order rows, columns (h d); [C, ldo) written as 0
+  const float* bias;              // [H][49][64] relative position bias * log2(e), -inf past 49
+  int B, R, nwx, C, H;            // images, resolution, windows per row (R / 7), channels, heads
+  int shift;                      // cyclic shift (0: W-MSA, 3: SW-MSA with the region mask)
+  float scale_log2;               // 32^-0.5 * log2(e)
+};
+hipError_t swin_patch_launch(int dtype, const float* img, int B, int C, int S, int ps, void* out,
+                             int ldo, hipStream_t s);
+hipError_t ln_rows_launch(int dtype, const void* x, int64_t ld, void* y, const float* gamma,
+                          const float* beta, int rows, int D, float eps, float* stats, int nslots,
+                          hipStream_t s);
+hipError_t merge_launch(int dtype, const void* x, int64_t ldx, int B, int R, int C, void* out,
+                        float* stats, int nslots, hipStream_t s);
+hipError_t rpb_dense_launch(const float* table, int H, int w, float* dense, hipStream_t s);
+hipError_t window_attn_launch(int dtype, const SwinAttnParams& p, hipStream_t s);
+hipError_t ln_pool_launch(int dtype, const void* x, int64_t ldx, int B, int T, int D,
+                          const float* stats, int nslots, const float* gamma, const float* beta,
+                          void* out, int64_t ldo, hipStream_t s);
 
 }  // namespace evt

@@ -165,6 +165,10 @@ __device__ __forceinline__ void epi_rows_t(const GemmParams& p, EVT_LDS char* st
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(v[j]);
     }
+    if (FL & EPI_GELU_ERF) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = gelu_erf(v[j]);
+    }
     if (FL & EPI_POS) {
       const int img = m / p.P, t = m - img * p.P;
       orow = (int64_t)img * (p.P + 1) + 1 + t;
@@ -290,11 +294,11 @@ __device__ __forceinline__ void epi_rows8_t(const GemmParams& p, EVT_LDS char* s
       v[0] += bias4[0];
       v[1] += bias4[1];
     }
-    if (FL & EPI_GELU) {
+    if (FL & (EPI_GELU | EPI_GELU_ERF)) {
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[h][j] = gelu_tanh(v[h][j]);
+        for (int j = 0; j < 4; ++j) v[h][j] = (FL & EPI_GELU) ? gelu_tanh(v[h][j]) : gelu_erf(v[h][j]);
     }
     if (FL & EPI_POS) {
       const int img = m / p.P, t = m - img * p.P;
@@ -943,13 +947,14 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
       }
     }
   }
-  if constexpr ((FL & EPI_GELU) != 0) {
+  if constexpr ((FL & (EPI_GELU | EPI_GELU_ERF)) != 0) {
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
       for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[nt][mt][j] = gelu_tanh(acc[nt][mt][j]);
+        for (int j = 0; j < 4; ++j)
+          acc[nt][mt][j] = (FL & EPI_GELU) ? gelu_tanh(acc[nt][mt][j]) : gelu_erf(acc[nt][mt][j]);
   }
   // 2. store layout: pair (2k, 2k+1) -> lane row wm*128 + (2k + (fg & 1))*16 + frow, columns
   //    wn*64 + nt*16 + (fg >> 1)*8 + [acc[nt][2k][0..3], acc[nt][2k+1][0..3]]
@@ -1327,7 +1332,9 @@ int num_cus() {
 constexpr bool pers_fl(int fl) {
   return fl == 0 || fl == EPI_BIAS || fl == (EPI_BIAS | EPI_GELU) || fl == (EPI_LNIN | EPI_BIAS) ||
          fl == (EPI_LNIN | EPI_BIAS | EPI_GELU) ||
-         fl == (EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS);
+         fl == (EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS) ||
+         fl == (EPI_LNIN | EPI_BIAS | EPI_GELU_ERF) || fl == (EPI_BIAS | EPI_RESID | EPI_STATS) ||
+         fl == (EPI_LNIN | EPI_BIAS | EPI_STATS);
 }
 
 // persistent kernel: supported epilogue, 8-column output groups, LN rows of <= 8 slots
@@ -1413,6 +1420,9 @@ hipError_t dispatch(int flags, const GemmParams& p, hipStream_t s) {
     EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_GELU)                 // LN2-folded FC1 + GELU
     EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_OUT_F32)              // LN-folded classifier (T2T)
     EVT_CASE(EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS)   // out-proj / FC2 + LN residual
+    EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_GELU_ERF)             // Swin LN2-folded FC1 + erf GELU
+    EVT_CASE(EPI_BIAS | EPI_RESID | EPI_STATS)               // Swin proj / FC2 + plain residual
+    EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_STATS)                // Swin LN-folded patch-merge reduction
 #undef EVT_CASE
     default: return hipErrorInvalidValue;
   }

@@ -1,0 +1,488 @@
+// Swin Transformer kernels for gfx950 (reference `utils.py:14-47` get_swin -> microsoft
+// Swin-Transformer `SwinTransformer`, benchmarked as swin_tiny_patch4_window7_224 NCHW by
+// `tools.py:272-282`; the algorithm restated in oracle/swin_ref.py).
+//
+// The token stream stays in raster order [B][R*R][Cst] (Cst = C rounded up to 64, pad columns
+// kept at exactly 0) for the whole stage: LayerNorm, QKV, proj and the MLP are per-token, so the
+// cyclic shift and the window partition / reverse only change WHICH rows one window's attention
+// reads and writes. window_attn_* computes those row indices itself (torch.roll(-s) + 7x7
+// partition on the way in, the inverse on the way out) - no roll, partition or reverse pass ever
+// touches HBM.
+//
+//   swin_patch_kernel    Conv2d(k = s = patch) as im2col: NCHW fp32 -> rows (c, kh, kw), zero pad
+//   ln_rows_kernel       LayerNorm of act-dtype rows -> act dtype + slot statistics (embed norm)
+//   merge_kernel         PatchMerging gather x[0::2,0::2] | x[1::2,0::2] | x[0::2,1::2] |
+//                        x[1::2,1::2] -> [B*(R/2)^2][4C] + row statistics (its LayerNorm is folded
+//                        into the reduction GEMM)
+//   window_attn_bf16     one wave per (window, head): S^T = K Q^T and O^T = V^T P^T on
+//                        v_mfma_f32_16x16x32_bf16 (head size 32 = one MFMA k-step), + relative
+//                        position bias, + SW-MSA mask from the region ids, exact softmax
+//   window_attn_f32      the exact fp32 parity path (VALU dot products, K / V in LDS)
+//   ln_pool_kernel       final LayerNorm + mean over tokens (AdaptiveAvgPool1d) -> [B][Cst]
+#include <algorithm>
+
+#include "common.h"
+#include "evt_internal.h"
+
+namespace evt {
+
+namespace {
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+// ---- patch embedding im2col ----------------------------------------------------------------
+template <typename TO>
+__global__ __launch_bounds__(256) void swin_patch_kernel(const float* __restrict__ img, int B,
+                                                         int C, int S, int ps,
+                                                         TO* __restrict__ out, int ldo) {
+  const int np = S / ps, pd = C * ps * ps;
+  const int64_t total = (int64_t)B * np * np * ldo;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t row = e / ldo;
+    const int f = (int)(e - row * ldo);
+    float v = 0.f;
+    if (f < pd) {
+      const int b = (int)(row / (np * np)), t = (int)(row - (int64_t)b * np * np);
+      const int py = t / np, px = t - py * np;
+      const int c = f / (ps * ps), r = f - c * ps * ps, kh = r / ps, kw = r - kh * ps;
+      v = img[(((int64_t)b * C + c) * S + py * ps + kh) * S + px * ps + kw];
+    }
+    out[e] = from_f32<TO>(v);
+  }
+}
+
+// ---- LayerNorm rows (act dtype in / out) + statistics of the stored output -----------------
+template <typename T, int NV>
+__global__ __launch_bounds__(256) void ln_rows_kernel(const T* __restrict__ x, int64_t ld,
+                                                      T* __restrict__ y,
+                                                      const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, int rows,
+                                                      int D, float eps,
+                                                      float* __restrict__ stats, int nslots) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const T* xr = x + (int64_t)row * ld;
+  float v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = i * 64 + lane;
+    v[i] = c < D ? to_f32(xr[c]) : 0.f;
+    s += v[i];
+  }
+  const float inv_d = 1.0f / (float)D;
+  const float mean = wave_sum(s) * inv_d;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = i * 64 + lane;
+    if (c < D) q += (v[i] - mean) * (v[i] - mean);
+  }
+  const float rstd = rsqrtf(wave_sum(q) * inv_d + eps);
+  T* yr = y + (int64_t)row * ld;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = i * 64 + lane;
+    if (c < ld) {
+      const T o = from_f32<T>(c < D ? (v[i] - mean) * rstd * gamma[c] + beta[c] : 0.f);
+      yr[c] = o;
+      const float f = to_f32(o);
+      s1 += f;
+      s2 += f * f;
+    }
+  }
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if (lane < nslots) {
+    float* st = stats + 2 * ((int64_t)nslots * row + lane);
+    st[0] = lane == 0 ? s1 : 0.f;
+    st[1] = lane == 0 ? s2 : 0.f;
+  }
+}
+
+// ---- PatchMerging gather: one wave per output row ------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void merge_kernel(const T* __restrict__ x, int64_t ldx, int B,
+                                                    int R, int C, T* __restrict__ out,
+                                                    float* __restrict__ stats, int nslots) {
+  const int lane = threadIdx.x & 63;
+  const int64_t orow = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int R2 = R / 2;
+  if (orow >= (int64_t)B * R2 * R2) return;
+  const int b = (int)(orow / (R2 * R2)), t = (int)(orow - (int64_t)b * R2 * R2);
+  const int oy = t / R2, ox = t - oy * R2;
+  T* op = out + orow * 4 * C;
+  float s1 = 0.f, s2 = 0.f;
+  // quadrant q: (dy, dx) = (q & 1, q >> 1) (reference order x0, x1, x2, x3)
+  for (int e = lane; e < 4 * C; e += 64) {
+    const int q = e / C, c = e - q * C;
+    const int y = 2 * oy + (q & 1), xx = 2 * ox + (q >> 1);
+    const T v = x[((int64_t)b * R * R + (int64_t)y * R + xx) * ldx + c];
+    op[e] = v;
+    const float f = to_f32(v);
+    s1 += f;
+    s2 += f * f;
+  }
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if (lane < nslots) {
+    float* st = stats + 2 * ((int64_t)nslots * orow + lane);
+    st[0] = lane == 0 ? s1 : 0.f;
+    st[1] = lane == 0 ? s2 : 0.f;
+  }
+}
+
+// ---- relative position bias, expanded once per block at model creation ----------------------
+// dense[h][q][k] = table[(qy-ky+w-1)*(2w-1) + (qx-kx+w-1)][h] * log2(e) for k < w*w, -inf after.
+__global__ void rpb_dense_kernel(const float* __restrict__ table, int H, int w,
+                                 float* __restrict__ dense) {
+  const int n = w * w;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= H * n * 64) return;
+  const int h = e / (n * 64), r = e - h * n * 64, q = r / 64, k = r - q * 64;
+  float v = -INFINITY;
+  if (k < n) {
+    const int qy = q / w, qx = q - qy * w, ky = k / w, kx = k - ky * w;
+    v = table[((qy - ky + w - 1) * (2 * w - 1) + (qx - kx + w - 1)) * H + h] * kLog2e;
+  }
+  dense[e] = v;
+}
+
+// Row of window-local token t (t < 49) of window `win` of image b, with the cyclic shift; and
+// its SW-MSA region id (3x3 regions of the shifted frame).
+struct WinGeom {
+  int R, nwx, s;
+  __device__ __forceinline__ int64_t row(int b, int win, int t) const {
+    const int wy = win / nwx, wx = win - wy * nwx;
+    const int i = t / 7, j = t - i * 7;
+    int y = wy * 7 + i + s, x = wx * 7 + j + s;
+    if (y >= R) y -= R;
+    if (x >= R) x -= R;
+    return (int64_t)b * R * R + (int64_t)y * R + x;
+  }
+  __device__ __forceinline__ int region(int win, int t) const {
+    const int wy = win / nwx, wx = win - wy * nwx;
+    const int i = t / 7, j = t - i * 7;
+    const int ys = wy * 7 + i, xs = wx * 7 + j;
+    const int rh = ys < R - 7 ? 0 : (ys < R - s ? 1 : 2);
+    const int rw = xs < R - 7 ? 0 : (xs < R - s ? 1 : 2);
+    return rh * 3 + rw;
+  }
+};
+
+// bf16 window attention. 4 waves per block, wave = one (image, window, head); head size 32,
+// window 7x7 = 49 tokens padded to 64 (4 tiles of 16). Q / K fragments are 16-B loads straight
+// from the QKV rows; V goes to the wave's 4 KiB of LDS (glds, chunk swizzle (row >> 2) & 3) for
+// the transposed ds_read_b64_tr_b16 reads of the V^T operand.
+__global__ __launch_bounds__(256) void window_attn_bf16_kernel(SwinAttnParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * 64 * 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t pair = (int64_t)blockIdx.x * 4 + wave;
+  const int nw = p.nwx * p.nwx;
+  if (pair >= (int64_t)p.B * nw * p.H) return;
+  const int h = (int)(pair % p.H);
+  const int64_t bw = pair / p.H;
+  const int win = (int)(bw % nw), b = (int)(bw / nw);
+  const WinGeom G{p.R, p.nwx, p.shift};
+  const bf16* qkv = (const bf16*)p.qkv;
+  const int g = lane >> 4, c16 = lane & 15;
+  EVT_LDS char* Vs = (EVT_LDS char*)smem + wave * 4096;
+
+  // V rows (keys) -> LDS: instruction i covers rows 16 i + (lane >> 2), 16-B chunk lane & 3
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 16 * i + (lane >> 2), ch = (lane & 3) ^ ((r >> 2) & 3);
+    const int64_t gr = G.row(b, win, min(r, 48));
+    glds16(qkv + gr * p.ldq + 2 * p.C + h * 32 + ch * 8, Vs + i * 1024);
+  }
+  // Q and K fragments: tile i, lane (token 16 i + c16, d 8 g .. 8 g + 7)
+  u32x4 qf[4], kf[4];
+  int64_t qrow[4];
+  int qreg[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int t = min(16 * i + c16, 48);
+    qrow[i] = G.row(b, win, t);
+    qreg[i] = G.region(win, t);
+    const bf16* rp = qkv + qrow[i] * p.ldq + h * 32 + 8 * g;
+    qf[i] = *(const u32x4*)rp;
+    kf[i] = *(const u32x4*)(rp + p.C);
+  }
+  // key regions of this lane's 16 keys (key 16 kt + 4 g + j)
+  int kreg[4][4];
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) kreg[kt][j] = G.region(win, min(16 * kt + 4 * g + j, 48));
+  wait_vmcnt0();
+
+  const float mval = -100.0f * kLog2e;
+  const float* bias_h = p.bias + (int64_t)h * 49 * 64;
+  const int tq = (lane >> 2) & 3, tp = lane & 3;
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    const int q = 16 * qt + c16;
+    f32x4 s[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf[kt]),
+                                                      __builtin_bit_cast(bf16x8, qf[qt]), acc, 0,
+                                                      0, 0);
+    }
+    // s[kt][j] = S^T[key 16 kt + 4 g + j][query q]: scores in the log2 domain + bias (+ mask)
+    const float* br = bias_h + (int64_t)min(q, 48) * 64 + 4 * g;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      const f32x4 bv = *(const f32x4*)(br + 16 * kt);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v = s[kt][j] * p.scale_log2 + bv[j];
+        if (p.shift && kreg[kt][j] != qreg[qt]) v += mval;
+        s[kt][j] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float e = __builtin_amdgcn_exp2f(s[kt][j] - mx);
+        s[kt][j] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+
+    f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 pf;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pf[j] = (bf16)s[2 * ks][j];
+        pf[4 + j] = (bf16)s[2 * ks + 1][j];
+      }
+      const int key0 = ks * 32 + 4 * g + tq;  // and key0 + 16: same (row >> 2) & 3 swizzle
+      const int sw = (key0 >> 2) & 3;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int chunk = 2 * dt + (tp >> 1);
+        const int off = ((chunk ^ sw) * 16) + (tp & 1) * 8;
+        const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((EVT_LDS i16x4*)(Vs + key0 * 64 + off));
+        const i16x4 v1 =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((EVT_LDS i16x4*)(Vs + (key0 + 16) * 64 + off));
+        const i16x8 vv = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[dt],
+                                                        0, 0, 0);
+      }
+    }
+    // o[dt][j] = O^T[d = 16 dt + 4 g + j][query q]
+    if (q < 49) {
+      const float inv = 1.0f / sum;
+      bf16* op = (bf16*)p.out + qrow[qt] * p.ldo;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) store4(op + h * 32 + 16 * dt + 4 * g, o[dt] * inv);
+      if (h == 0)  // pad columns [C, ldo) of the attention output (the proj GEMM's K padding)
+        for (int c = p.C + 4 * g; c < p.ldo; c += 16) store4(op + c, f32x4{0.f, 0.f, 0.f, 0.f});
+    }
+  }
+}
+
+// fp32 window attention (parity path): wave = (image, window, head), lane = query (49 of 64).
+__global__ __launch_bounds__(256) void window_attn_f32_kernel(SwinAttnParams p) {
+  __shared__ float smem[4][2][49][33];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t pair = (int64_t)blockIdx.x * 4 + wave;
+  const int nw = p.nwx * p.nwx;
+  if (pair >= (int64_t)p.B * nw * p.H) return;
+  const int h = (int)(pair % p.H);
+  const int64_t bw = pair / p.H;
+  const int win = (int)(bw % nw), b = (int)(bw / nw);
+  const WinGeom G{p.R, p.nwx, p.shift};
+  const float* qkv = (const float*)p.qkv;
+  float(*Ks)[33] = smem[wave][0];
+  float(*Vs)[33] = smem[wave][1];
+  for (int e = lane; e < 49 * 32; e += 64) {
+    const int t = e >> 5, d = e & 31;
+    const float* rp = qkv + G.row(b, win, t) * p.ldq + h * 32 + d;
+    Ks[t][d] = rp[p.C];
+    Vs[t][d] = rp[2 * p.C];
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // wave-private LDS: no barrier
+  __builtin_amdgcn_wave_barrier();
+  const int t = min(lane, 48);
+  const int64_t qrow = G.row(b, win, t);
+  const int qreg = G.region(win, t);
+  float q[32];
+#pragma unroll
+  for (int d = 0; d < 32; ++d) q[d] = qkv[qrow * p.ldq + h * 32 + d];
+  const float* br = p.bias + ((int64_t)h * 49 + t) * 64;
+  float sc[49];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < 49; ++k) {
+    float a = 0.f;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) a += q[d] * Ks[k][d];
+    float v = a * p.scale_log2 + br[k];
+    if (p.shift && G.region(win, k) != qreg) v += -100.0f * kLog2e;
+    sc[k] = v;
+    mx = fmaxf(mx, v);
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < 49; ++k) {
+    sc[k] = exp2f(sc[k] - mx);
+    sum += sc[k];
+  }
+  float o[32];
+#pragma unroll
+  for (int d = 0; d < 32; ++d) o[d] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 49; ++k)
+#pragma unroll
+    for (int d = 0; d < 32; ++d) o[d] += sc[k] * Vs[k][d];
+  if (lane < 49) {
+    float* op = (float*)p.out + qrow * p.ldo;
+    const float inv = 1.0f / sum;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) op[h * 32 + d] = o[d] * inv;
+    if (h == 0)
+      for (int c = p.C; c < p.ldo; ++c) op[c] = 0.f;
+  }
+}
+
+// ---- final LayerNorm + token mean: one block per image -------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void ln_pool_kernel(const T* __restrict__ x, int64_t ldx, int T_,
+                                                      int D, const float* __restrict__ stats,
+                                                      int nslots, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, float eps,
+                                                      T* __restrict__ out, int64_t ldo) {
+  __shared__ float coef[256][2];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float inv_d = 1.0f / (float)D;
+  for (int t = tid; t < T_; t += 256) {
+    const float* st = stats + 2 * (int64_t)nslots * ((int64_t)b * T_ + t);
+    float s1 = 0.f, s2 = 0.f;
+    for (int j = 0; j < nslots; ++j) {
+      s1 += st[2 * j];
+      s2 += st[2 * j + 1];
+    }
+    const float mu = s1 * inv_d;
+    coef[t][0] = mu;
+    coef[t][1] = rsqrtf(fmaxf(s2 * inv_d - mu * mu, 0.f) + eps);
+  }
+  __syncthreads();
+  const T* xb = x + (int64_t)b * T_ * ldx;
+  for (int c = tid; c < ldo; c += 256) {
+    float acc = 0.f;
+    if (c < D)
+      for (int t = 0; t < T_; ++t) acc += (to_f32(xb[(int64_t)t * ldx + c]) - coef[t][0]) * coef[t][1];
+    out[(int64_t)b * ldo + c] = from_f32<T>(c < D ? acc / (float)T_ * gamma[c] + beta[c] : 0.f);
+  }
+}
+
+template <typename T>
+hipError_t ln_rows_t(const void* x, int64_t ld, void* y, const float* g, const float* bb, int rows,
+                     int D, float eps, float* stats, int nslots, hipStream_t s) {
+  const dim3 grid((rows + 3) / 4);
+  if (ld <= 128)
+    hipLaunchKernelGGL((ln_rows_kernel<T, 2>), grid, dim3(256), 0, s, (const T*)x, ld, (T*)y, g,
+                       bb, rows, D, eps, stats, nslots);
+  else if (ld <= 256)
+    hipLaunchKernelGGL((ln_rows_kernel<T, 4>), grid, dim3(256), 0, s, (const T*)x, ld, (T*)y, g,
+                       bb, rows, D, eps, stats, nslots);
+  else if (ld <= 512)
+    hipLaunchKernelGGL((ln_rows_kernel<T, 8>), grid, dim3(256), 0, s, (const T*)x, ld, (T*)y, g,
+                       bb, rows, D, eps, stats, nslots);
+  else
+    hipLaunchKernelGGL((ln_rows_kernel<T, 16>), grid, dim3(256), 0, s, (const T*)x, ld, (T*)y, g,
+                       bb, rows, D, eps, stats, nslots);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t swin_patch_launch(int dtype, const float* img, int B, int C, int S, int ps, void* out,
+                             int ldo, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  if (S % ps || C * ps * ps > ldo) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)B * (S / ps) * (S / ps) * ldo;
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, 65536);
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(swin_patch_kernel<bf16>, dim3(grid), dim3(256), 0, s, img, B, C, S, ps,
+                       (bf16*)out, ldo);
+  else
+    hipLaunchKernelGGL(swin_patch_kernel<float>, dim3(grid), dim3(256), 0, s, img, B, C, S, ps,
+                       (float*)out, ldo);
+  return hipGetLastError();
+}
+
+hipError_t ln_rows_launch(int dtype, const void* x, int64_t ld, void* y, const float* gamma,
+                          const float* beta, int rows, int D, float eps, float* stats, int nslots,
+                          hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  if (D <= 0 || D > ld || ld > 1024 || nslots > 64) return hipErrorInvalidValue;
+  return dtype == DT_BF16 ? ln_rows_t<bf16>(x, ld, y, gamma, beta, rows, D, eps, stats, nslots, s)
+                          : ln_rows_t<float>(x, ld, y, gamma, beta, rows, D, eps, stats, nslots, s);
+}
+
+hipError_t merge_launch(int dtype, const void* x, int64_t ldx, int B, int R, int C, void* out,
+                        float* stats, int nslots, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  if (R % 2 || C <= 0 || C > ldx || nslots > 64) return hipErrorInvalidValue;
+  const int64_t rows = (int64_t)B * (R / 2) * (R / 2);
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(merge_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, ldx, B, R, C,
+                       (bf16*)out, stats, nslots);
+  else
+    hipLaunchKernelGGL(merge_kernel<float>, grid, dim3(256), 0, s, (const float*)x, ldx, B, R, C,
+                       (float*)out, stats, nslots);
+  return hipGetLastError();
+}
+
+hipError_t rpb_dense_launch(const float* table, int H, int w, float* dense, hipStream_t s) {
+  const int n = H * w * w * 64;
+  hipLaunchKernelGGL(rpb_dense_kernel, dim3((n + 255) / 256), dim3(256), 0, s, table, H, w, dense);
+  return hipGetLastError();
+}
+
+hipError_t window_attn_launch(int dtype, const SwinAttnParams& p, hipStream_t s) {
+  if (p.B <= 0) return hipSuccess;
+  if (p.R % 7 || p.nwx * 7 != p.R || p.C != p.H * 32 || p.ldo < p.C || p.shift < 0 ||
+      p.shift >= 7 || (p.ldq % 8) || (p.ldo % 4))
+    return hipErrorInvalidValue;
+  const int64_t pairs = (int64_t)p.B * p.nwx * p.nwx * p.H;
+  const dim3 grid((unsigned)((pairs + 3) / 4));
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(window_attn_bf16_kernel, grid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(window_attn_f32_kernel, grid, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t ln_pool_launch(int dtype, const void* x, int64_t ldx, int B, int T, int D,
+                          const float* stats, int nslots, const float* gamma, const float* beta,
+                          void* out, int64_t ldo, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  if (T <= 0 || T > 256 || D > ldo) return hipErrorInvalidValue;
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(ln_pool_kernel<bf16>, dim3(B), dim3(256), 0, s, (const bf16*)x, ldx, T, D,
+                       stats, nslots, gamma, beta, 1e-5f, (bf16*)out, ldo);
+  else
+    hipLaunchKernelGGL(ln_pool_kernel<float>, dim3(B), dim3(256), 0, s, (const float*)x, ldx, T, D,
+                       stats, nslots, gamma, beta, 1e-5f, (float*)out, ldo);
+  return hipGetLastError();
+}
+
+}  // namespace evt

@@ -288,3 +288,126 @@ def digest(arrays: Dict[str, np.ndarray] | Sequence[np.ndarray]) -> str:
         h.update(str(k).encode())
         h.update(np.ascontiguousarray(v).tobytes())
     return h.hexdigest()
+
+
+@dataclass(frozen=True)
+class SwinConfig:
+    """Static shape of a Swin Transformer, the model the reference builds with `get_swin`
+    (`utils.py:14-47`, config `swin_tiny_patch4_window7_224`, `tools.py:282`) from the external
+    microsoft/Swin-Transformer repo (not vendored in the reference). Stage i has embed_dim * 2^i
+    channels, num_heads[i] heads of size 32, depths[i] blocks alternating W-MSA / SW-MSA
+    (shift window_size // 2), and a PatchMerging in front of every stage but the first.
+    """
+
+    image_size: int = 224
+    patch_size: int = 4
+    in_chans: int = 3
+    num_classes: int = 1000
+    embed_dim: int = 96
+    depths: Sequence[int] = (2, 2, 6, 2)
+    num_heads: Sequence[int] = (3, 6, 12, 24)
+    window_size: int = 7
+    mlp_ratio: float = 4.0
+
+    @property
+    def num_stages(self) -> int:
+        return len(self.depths)
+
+    def dim(self, i: int) -> int:
+        return self.embed_dim * (1 << i)
+
+    def res(self, i: int) -> int:
+        return self.image_size // self.patch_size // (1 << i)
+
+    def window(self, i: int) -> int:
+        """Window of stage i: clamped to the resolution when that is not larger (the reference
+        Swin's `min(input_resolution) <= window_size` rule: no shift then)."""
+        return min(self.window_size, self.res(i))
+
+    def shift(self, i: int, j: int) -> int:
+        return 0 if (j % 2 == 0 or self.res(i) <= self.window_size) else self.window_size // 2
+
+    def mlp(self, i: int) -> int:
+        return int(self.dim(i) * self.mlp_ratio)
+
+    @property
+    def num_features(self) -> int:
+        return self.dim(self.num_stages - 1)
+
+    def gflop_per_image(self) -> float:
+        """Matmul FLOPs (2*MAC) per image: patch embed, QKV / window attention / proj / MLP,
+        patch merging, head (the MAC terms of the reference's `SwinFlops`,
+        flops_calculation.py:313-386)."""
+        f = 2.0 * self.res(0) ** 2 * self.in_chans * self.patch_size ** 2 * self.embed_dim
+        for i in range(self.num_stages):
+            n, c, w = self.res(i) ** 2, self.dim(i), self.window(i)
+            per = 2.0 * n * c * 3 * c + 2.0 * 2 * n * w * w * c + 2.0 * n * c * c \
+                + 2.0 * 2 * n * c * self.mlp(i)
+            f += self.depths[i] * per
+            if i + 1 < self.num_stages:
+                f += 2.0 * (n // 4) * 4 * c * 2 * c
+        f += 2.0 * self.num_features * self.num_classes
+        return f / 1e9
+
+
+SWIN_VARIANTS = {  # microsoft/Swin-Transformer configs/swin_{tiny,small,base}_patch4_window7_224.yaml
+    "tiny": dict(embed_dim=96, depths=(2, 2, 6, 2), num_heads=(3, 6, 12, 24)),
+    "small": dict(embed_dim=96, depths=(2, 2, 18, 2), num_heads=(3, 6, 12, 24)),
+    "base": dict(embed_dim=128, depths=(2, 2, 18, 2), num_heads=(4, 8, 16, 32)),
+}
+
+
+def swin_config(variant: str = "tiny", **kw) -> SwinConfig:
+    args = dict(SWIN_VARIANTS[variant])
+    args.update(kw)
+    args["depths"] = tuple(args["depths"])
+    args["num_heads"] = tuple(args["num_heads"])
+    return SwinConfig(**args)
+
+
+def swin_param_shapes(cfg: SwinConfig) -> List[tuple]:
+    """Ordered (name, shape) list = the C-ABI weight order of evt_swin_create (include/evt.h).
+    Dense kernels are [in, out]; `patch_w` is the Conv2d(k=s=patch) kernel flattened to rows
+    (c, kh, kw); `rpb` is the relative-position-bias table [(2w-1)^2, heads]."""
+    e, p = cfg.embed_dim, cfg.patch_size
+    out = [("patch_w", (cfg.in_chans * p * p, e)), ("patch_b", (e,)),
+           ("pnorm_g", (e,)), ("pnorm_b", (e,))]
+    for i in range(cfg.num_stages):
+        c, h, w = cfg.dim(i), cfg.num_heads[i], cfg.window(i)
+        if i > 0:
+            cp = cfg.dim(i - 1)
+            out += [(f"s{i}.merge_g", (4 * cp,)), (f"s{i}.merge_b", (4 * cp,)),
+                    (f"s{i}.merge_w", (4 * cp, c))]
+        for j in range(cfg.depths[i]):
+            pre = f"s{i}.b{j}."
+            out += [(pre + "ln1_g", (c,)), (pre + "ln1_b", (c,)),
+                    (pre + "qkv_w", (c, 3 * c)), (pre + "qkv_b", (3 * c,)),
+                    (pre + "rpb", ((2 * w - 1) ** 2, h)),
+                    (pre + "proj_w", (c, c)), (pre + "proj_b", (c,)),
+                    (pre + "ln2_g", (c,)), (pre + "ln2_b", (c,)),
+                    (pre + "fc1_w", (c, cfg.mlp(i))), (pre + "fc1_b", (cfg.mlp(i),)),
+                    (pre + "fc2_w", (cfg.mlp(i), c)), (pre + "fc2_b", (c,))]
+    nf = cfg.num_features
+    out += [("norm_g", (nf,)), ("norm_b", (nf,)), ("head_w", (nf, cfg.num_classes)),
+            ("head_b", (cfg.num_classes,))]
+    return out
+
+
+def make_swin_params(cfg: SwinConfig, seed: int = 0) -> Dict[str, np.ndarray]:
+    """Seeded fp32 Swin parameters (families as make_vit_params; the relative-position-bias
+    tables ~ N(0, 0.5), wider than the reference's trunc_normal(0.02) so that a wrong bias index
+    shows in the logits)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    params: Dict[str, np.ndarray] = {}
+    for name, shape in swin_param_shapes(cfg):
+        leaf = name.split(".")[-1]
+        if leaf == "rpb":
+            v = rng.normal(0.0, 0.5, size=shape)
+        elif leaf.endswith("_w"):
+            v = _glorot(rng, shape[0], shape[1])
+        elif leaf.endswith("_g"):
+            v = 1.0 + rng.normal(0.0, 0.02, size=shape)
+        else:  # biases, LN beta
+            v = rng.normal(0.0, 0.02, size=shape)
+        params[name] = np.ascontiguousarray(v, dtype=np.float32)
+    return params

@@ -130,6 +130,7 @@ int evt_ln_fold(int dtype, const void* Wp, int Kpad, int Npad, const float* W, c
 #define EVT_EPI_LNIN 32    /* A rows un-normalised: r*acc - r*mu*colsum[n] (+ bias = cvec) */
 #define EVT_EPI_RESLN 64   /* residual is LN(resid) with rstats / rgamma / rbeta (norm.py:12) */
 #define EVT_EPI_STATS 128  /* write per-slab (sum, sumsq) of each stored row into stats_out */
+#define EVT_EPI_GELU_ERF 256 /* exact erf GELU (torch nn.GELU, the Swin MLP) */
 /* LayerNorm row statistics layout: float stats[rows][S][2], S = 2 * ceil(ln_width / 256) slots
  * (one per 128-column slab); a row's (sum, sumsq) is the sum over its S slots. */
 
@@ -156,7 +157,8 @@ typedef struct evt_dense_args {
 /* Dense layer on the token matrix: C = epi(A . W) (reference tf.keras.layers.Dense), one of the
  * flag sets 0, 1, 3, 17, 21, 25, 137 (patch embed -> stream), 33 (LN-folded QKV),
  * 35 (LN-folded FC1 + GELU), 49 (LN-folded classifier, fp32 logits), 197 (out-proj / FC2 + LN
- * residual + stats). */
+ * residual + stats); Swin: 289 (LN-folded FC1 + erf GELU), 133 (proj / FC2 + residual + stats),
+ * 161 (LN-folded patch-merge reduction + stats). */
 int evt_dense(int dtype, const evt_dense_args* args, void* stream);
 
 /* Multi-head attention core (attention.py:20-34): qkv [B*N, ldq] with columns (qkv h d), head
@@ -233,6 +235,66 @@ int evt_performer(int dtype, const void* kqv, int64_t ldq, int B, int T, const f
 
 /* fp32 scratch elements evt_performer needs for B images of T tokens. */
 int64_t evt_performer_scratch(int B, int T);
+
+/* ---- Swin Transformer (reference utils.py:14-47 get_swin -> microsoft SwinTransformer) ---- */
+
+#define EVT_SWIN_MAX_STAGES 8
+
+/* Static shape of a SwinTransformer(img_size, patch_size, in_chans, num_classes, embed_dim, depths,
+ * num_heads, window_size, mlp_ratio, qkv_bias=True, ape=False, patch_norm=True) as get_swin builds
+ * it (utils.py:28-43; swin_tiny_patch4_window7_224 = embed 96, depths (2,2,6,2), heads
+ * (3,6,12,24)). This build: window 7, head size 32 (stage width / heads), every stage resolution
+ * a multiple of 7 (no padding), stage width <= 1024. */
+typedef struct evt_swin_desc {
+  int32_t image_size;   /* 224 */
+  int32_t patch_size;   /* 4 */
+  int32_t in_chans;     /* 3 */
+  int32_t num_classes;  /* 1000 */
+  int32_t embed_dim;    /* 96; stage i has embed_dim << i channels */
+  int32_t num_stages;   /* len(depths), <= EVT_SWIN_MAX_STAGES */
+  int32_t depths[EVT_SWIN_MAX_STAGES];
+  int32_t num_heads[EVT_SWIN_MAX_STAGES];
+  int32_t window_size;  /* 7 */
+  float mlp_ratio;      /* 4.0: MLP width int(C * mlp_ratio) */
+  int32_t dtype;        /* EVT_DTYPE_* */
+  int32_t max_batch;
+} evt_swin_desc;
+
+/* Number of fp32 weight tensors evt_swin_create expects, in order:
+ *   patch_w [in_chans*p*p, E] (Conv2d kernel, rows (c, kh, kw)), patch_b [E], pnorm_g [E], pnorm_b [E],
+ *   per stage i (width C): if i > 0: merge_g [2C], merge_b [2C], merge_w [2C, C] (LayerNorm(4C') +
+ *     reduction Linear(4C', 2C', bias=False) of PatchMerging, C' = C / 2);
+ *     per block: ln1_g [C], ln1_b [C], qkv_w [C, 3C] (columns (qkv h d)), qkv_b [3C],
+ *       rpb [169, heads] (relative_position_bias_table), proj_w [C, C], proj_b [C], ln2_g [C],
+ *       ln2_b [C], fc1_w [C, M], fc1_b [M], fc2_w [M, C], fc2_b [C]   (M = int(C * mlp_ratio))
+ *   norm_g [F], norm_b [F], head_w [F, classes], head_b [classes]   (F = last stage width).
+ * Dense kernels are [in, out] (the transpose of a torch Linear weight). */
+int evt_swin_num_weights(const evt_swin_desc* desc);
+
+/* Build a Swin model (same ownership rules as evt_vit_create). */
+int evt_swin_create(const evt_swin_desc* desc, const float* const* weights, int n_weights,
+                    void* stream, evt_model** out);
+
+/* Forward (SwinTransformer.forward): img fp32 NCHW [batch, in_chans, S, S] -> logits fp32
+ * [batch, num_classes]. Asynchronous on `stream`. */
+int evt_swin_forward(evt_model* model, const float* img, int batch, float* logits, void* stream);
+
+/* Bytes of device workspace evt_swin_create allocates for `batch` images. */
+int evt_swin_query_workspace(const evt_swin_desc* desc, int batch, size_t* bytes);
+
+/* (Shifted-)window multi-head self-attention core of one Swin block (WindowAttention + the
+ * cyclic shift / window partition / reverse around it): qkv [B*R*R, ldq] raster-order token rows
+ * with columns (qkv h d) (the qkv Linear output incl. bias), head size 32, window 7, cyclic shift
+ * `shift` (0 = W-MSA; else SW-MSA with the -100 region mask) -> out [B*R*R, ldo] raster rows,
+ * columns (h d), columns [C, ldo) set to 0. rpb = relative_position_bias_table [169, H]. */
+int evt_window_attention(int dtype, const void* qkv, int64_t ldq, void* out, int64_t ldo,
+                         const float* rpb, int B, int R, int C, int H, int shift, void* stream);
+
+/* PatchMerging gather: x [B, R, R, ldx] (C used) -> out [B*(R/2)^2, 4C] in the order
+ * x[0::2,0::2] | x[1::2,0::2] | x[0::2,1::2] | x[1::2,1::2]; each row's (sum, sumsq) goes to slot
+ * 0 of stats[row][nslots][2] (other slots zeroed). */
+int evt_patch_merge(int dtype, const void* x, int64_t ldx, int B, int R, int C, void* out,
+                    float* stats, int nslots, void* stream);
 
 #ifdef __cplusplus
 }

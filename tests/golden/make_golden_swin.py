@@ -1,0 +1,119 @@
+"""Generate the Swin golden fixtures (tests/golden/swin_*.npz).
+
+Run in the build container only:
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_swin.py
+
+The reference's Swin (`utils.py:14-47` get_swin) lives in an external, unvendored checkout of
+microsoft/Swin-Transformer, so there is no reference code to run. The golden logits come from the
+third-party HuggingFace `transformers` 5.15.0 `SwinForImageClassification`, an independent
+implementation of the same published model, built offline from a local `SwinConfig` (no download)
+and run in float64 on the seeded parameters of `edgevisiontransformer_amd.weights` mapped onto
+its state dict. Only data is stored (seeds, digests, logits, the embed checkpoint).
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.dont_write_bytecode = True
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+from edgevisiontransformer_amd.weights import digest, make_images, make_swin_params, swin_config  # noqa: E402
+from oracle.swin_ref import swin_forward  # noqa: E402
+
+CASES = {
+    # name: (config kwargs, batch, param seed, image seed)
+    "swin_tiny_b1": (dict(variant="tiny"), 1, 11, 12),
+    "swin_micro_b2": (dict(variant="tiny", image_size=56, depths=(2, 2), num_heads=(3, 6),
+                           num_classes=37), 2, 13, 14),
+}
+
+
+def hf_state_dict(params, cfg):
+    """Map the Keras-layout parameters onto HF Swin names ([out, in] Linear weights)."""
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64))  # noqa: E731
+    e, p = cfg.embed_dim, cfg.patch_size
+    sd = {
+        "swin.embeddings.patch_embeddings.projection.weight":
+            t(params["patch_w"].T.reshape(e, cfg.in_chans, p, p)),
+        "swin.embeddings.patch_embeddings.projection.bias": t(params["patch_b"]),
+        "swin.embeddings.norm.weight": t(params["pnorm_g"]),
+        "swin.embeddings.norm.bias": t(params["pnorm_b"]),
+        "swin.layernorm.weight": t(params["norm_g"]),
+        "swin.layernorm.bias": t(params["norm_b"]),
+        "classifier.weight": t(params["head_w"].T),
+        "classifier.bias": t(params["head_b"]),
+    }
+    for i in range(cfg.num_stages):
+        c = cfg.dim(i)
+        if i > 0:  # HF attaches the merge of stage i to the end of stage i-1
+            pre = f"swin.encoder.layers.{i - 1}.downsample."
+            sd[pre + "norm.weight"] = t(params[f"s{i}.merge_g"])
+            sd[pre + "norm.bias"] = t(params[f"s{i}.merge_b"])
+            sd[pre + "reduction.weight"] = t(params[f"s{i}.merge_w"].T)
+        for j in range(cfg.depths[i]):
+            src = f"s{i}.b{j}."
+            dst = f"swin.encoder.layers.{i}.blocks.{j}."
+            qw, qb = params[src + "qkv_w"], params[src + "qkv_b"]
+            for s, nm in enumerate("qkv"):
+                sd[dst + f"attention.{nm}_proj.weight"] = t(qw[:, s * c:(s + 1) * c].T)
+                sd[dst + f"attention.{nm}_proj.bias"] = t(qb[s * c:(s + 1) * c])
+            sd[dst + "attention.o_proj.weight"] = t(params[src + "proj_w"].T)
+            sd[dst + "attention.o_proj.bias"] = t(params[src + "proj_b"])
+            sd[dst + "attention.relative_position_bias.relative_position_bias_table"] = t(params[src + "rpb"])
+            sd[dst + "layernorm_before.weight"] = t(params[src + "ln1_g"])
+            sd[dst + "layernorm_before.bias"] = t(params[src + "ln1_b"])
+            sd[dst + "layernorm_after.weight"] = t(params[src + "ln2_g"])
+            sd[dst + "layernorm_after.bias"] = t(params[src + "ln2_b"])
+            sd[dst + "mlp.fc1.weight"] = t(params[src + "fc1_w"].T)
+            sd[dst + "mlp.fc1.bias"] = t(params[src + "fc1_b"])
+            sd[dst + "mlp.fc2.weight"] = t(params[src + "fc2_w"].T)
+            sd[dst + "mlp.fc2.bias"] = t(params[src + "fc2_b"])
+    return sd
+
+
+def hf_forward(params, cfg, img):
+    from transformers import SwinConfig, SwinForImageClassification
+    hc = SwinConfig(image_size=cfg.image_size, patch_size=cfg.patch_size, num_channels=cfg.in_chans,
+                    embed_dim=cfg.embed_dim, depths=list(cfg.depths), num_heads=list(cfg.num_heads),
+                    window_size=cfg.window_size, mlp_ratio=cfg.mlp_ratio, qkv_bias=True,
+                    hidden_act="gelu", layer_norm_eps=1e-5, drop_path_rate=0.0,
+                    num_labels=cfg.num_classes)
+    model = SwinForImageClassification(hc).to(torch.float64).eval()
+    missing, unexpected = model.load_state_dict(hf_state_dict(params, cfg), strict=False)
+    assert not unexpected, unexpected
+    assert all("relative_position_index" in k for k in missing), missing
+    with torch.no_grad():
+        out = model(pixel_values=torch.from_numpy(img.astype(np.float64))).logits
+    return out.numpy()
+
+
+def main():
+    for name, (kw, batch, pseed, iseed) in CASES.items():
+        kw = dict(kw)
+        cfg = swin_config(kw.pop("variant"), **kw)
+        params = make_swin_params(cfg, seed=pseed)
+        img = make_images(batch, seed=iseed, image_size=cfg.image_size, chans=cfg.in_chans)
+        logits = hf_forward(params, cfg, img)
+        trace = {}
+        ours = swin_forward(params, cfg, img, trace=trace)
+        err = float(np.abs(ours - logits).max())
+        print(f"{name}: |oracle - HF| = {err:.3e}, logits std {logits.std():.3f}")
+        assert err < 1e-9, err
+        np.savez_compressed(
+            os.path.join(HERE, f"{name}.npz"), logits=logits, embed=trace["embed"][:, :8],
+            param_seed=pseed, image_seed=iseed, batch=batch,
+            image_size=cfg.image_size, embed_dim=cfg.embed_dim, depths=np.array(cfg.depths),
+            num_heads=np.array(cfg.num_heads), num_classes=cfg.num_classes,
+            param_digest=digest(params), image_digest=digest([img]))
+
+
+if __name__ == "__main__":
+    main()

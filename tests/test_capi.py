@@ -27,7 +27,7 @@ def lib():
 def test_header_and_binding_agree():
     from edgevisiontransformer_amd import _lib
     assert _declared() == sorted(_lib.SIGNATURES)
-    assert len(_declared()) == 23
+    assert len(_declared()) == 29
 
 
 def test_every_declared_symbol_is_exported(lib):
@@ -85,3 +85,25 @@ def test_t2t_host_validation(lib):
     assert lib.evt_unfold(1, 1, None, 1, 8, 8, 3, 7, 4, 2, None, 147, None, 0, None) == _lib.EVT_EINVAL
     assert lib.evt_performer(1, None, 192, 1, 16, *([None] * 10), None, 64, None) == _lib.EVT_EINVAL
     assert lib.evt_performer_scratch(2, 3136) == 2 * 4 * (64 * 32 + 32)
+
+
+def test_swin_host_validation(lib):
+    from edgevisiontransformer_amd import _lib
+    from edgevisiontransformer_amd.modeling.models.swin import swin_config_from_name
+    from edgevisiontransformer_amd.weights import swin_param_shapes
+    cfg = swin_config_from_name("swin_tiny_patch4_window7_224")
+    d = _lib.evt_swin_desc()
+    d.image_size, d.patch_size, d.in_chans, d.num_classes = 224, 4, 3, 1000
+    d.embed_dim, d.num_stages, d.window_size, d.mlp_ratio = 96, 4, 7, 4.0
+    for i, (dp, h) in enumerate(zip((2, 2, 6, 2), (3, 6, 12, 24))):
+        d.depths[i], d.num_heads[i] = dp, h
+    d.dtype, d.max_batch = 1, 256
+    assert lib.evt_swin_num_weights(ctypes.byref(d)) == len(swin_param_shapes(cfg))
+    out = ctypes.c_size_t()
+    assert lib.evt_swin_query_workspace(ctypes.byref(d), 256, ctypes.byref(out)) == 0
+    assert 1e9 < out.value < 4e9
+    d.num_heads[0] = 4  # head size 24
+    assert lib.evt_swin_query_workspace(ctypes.byref(d), 256, ctypes.byref(out)) == _lib.EVT_EINVAL
+    assert b"head size" in lib.evt_last_error()
+    d.num_heads[0], d.image_size = 3, 192  # 48 -> stage resolutions not multiples of 7
+    assert lib.evt_swin_query_workspace(ctypes.byref(d), 256, ctypes.byref(out)) == _lib.EVT_EINVAL

@@ -1,0 +1,111 @@
+"""CPU: the Swin oracle (oracle/swin_ref.py) against the committed golden fixtures, which were
+produced by the third-party HuggingFace SwinForImageClassification in float64
+(tests/golden/make_golden_swin.py; the reference's own Swin lives in an unvendored external repo,
+so this pins the restatement to an independent implementation of the same model)."""
+import os
+
+import numpy as np
+import pytest
+
+from edgevisiontransformer_amd.weights import (SwinConfig, digest, make_images, make_swin_params,
+                                               swin_config, swin_param_shapes)
+from oracle import swin_ref
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def golden_case(name):
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    cfg = swin_config("tiny", image_size=int(z["image_size"]), embed_dim=int(z["embed_dim"]),
+                      depths=tuple(int(v) for v in z["depths"]),
+                      num_heads=tuple(int(v) for v in z["num_heads"]),
+                      num_classes=int(z["num_classes"]))
+    params = make_swin_params(cfg, seed=int(z["param_seed"]))
+    img = make_images(int(z["batch"]), seed=int(z["image_seed"]), image_size=cfg.image_size)
+    assert digest(params) == str(z["param_digest"])
+    assert digest([img]) == str(z["image_digest"])
+    return z, cfg, params, img
+
+
+@pytest.mark.parametrize("name", ["swin_micro_b2", "swin_tiny_b1"])
+def test_oracle_matches_golden(name):
+    z, cfg, params, img = golden_case(name)
+    trace = {}
+    out = swin_ref.swin_forward(params, cfg, img, trace=trace)
+    assert np.abs(out - z["logits"]).max() < 1e-9
+    assert np.abs(trace["embed"][:, :8] - z["embed"]).max() < 1e-12
+
+
+def test_swin_t_config_and_flops():
+    cfg = swin_config("tiny")
+    assert [cfg.dim(i) for i in range(4)] == [96, 192, 384, 768]
+    assert [cfg.res(i) for i in range(4)] == [56, 28, 14, 7]
+    assert [cfg.shift(3, j) for j in range(2)] == [0, 0]  # resolution == window: no shift
+    assert cfg.shift(0, 1) == 3 and cfg.shift(2, 5) == 3 and cfg.shift(2, 4) == 0
+    # ~4.5 GMAC (the reference's SwinFlops figure, flops_calculation.py:313-386) -> ~8.9 GFLOP
+    assert 8.7 < cfg.gflop_per_image() < 9.1
+    n = sum(int(np.prod(s)) for _, s in swin_param_shapes(cfg))
+    assert 28.2e6 < n < 28.4e6  # Swin-T: 28.3M parameters
+
+
+def test_shift_mask_and_bias_index():
+    idx = swin_ref.relative_position_index(7)
+    assert idx.shape == (49, 49) and idx.min() == 0 and idx.max() == 168
+    assert idx[0, 0] == 84 and idx[0, 48] == 0 and idx[48, 0] == 168
+    m = swin_ref.shift_mask(56, 56, 7, 3)
+    assert m.shape == (64, 49, 49)
+    assert not m[0].any()                      # interior window: one region
+    assert (m[63] != 0).sum() > 0 and set(np.unique(m)) == {0.0, -100.0}
+
+
+def test_window_attention_permutation_equivariance():
+    """Rolling the image by a full window commutes with W-MSA (a property the GPU test reuses)."""
+    rng = np.random.default_rng(0)
+    c, h, res = 64, 2, 14
+    y = rng.standard_normal((1, res * res, c))
+    w = {k: rng.standard_normal(s) * 0.2 for k, s in
+         (("qkv_w", (c, 3 * c)), ("qkv_b", (3 * c,)), ("rpb", (169, h)), ("proj_w", (c, c)),
+          ("proj_b", (c,)))}
+    out = swin_ref.window_attention(y, res, h, 7, 0, **w)
+    ys = np.roll(y.reshape(1, res, res, c), (7, 7), (1, 2)).reshape(1, -1, c)
+    outs = swin_ref.window_attention(ys, res, h, 7, 0, **w)
+    ref = np.roll(out.reshape(1, res, res, c), (7, 7), (1, 2)).reshape(1, -1, c)
+    assert np.abs(outs - ref).max() < 1e-12
+
+
+def test_state_dict_mapping_roundtrip():
+    from edgevisiontransformer_amd.modeling.models.swin import params_from_state_dict
+    cfg = swin_config("tiny", image_size=56, depths=(2, 2), num_heads=(3, 6), num_classes=37)
+    p = make_swin_params(cfg, seed=3)
+    e = cfg.embed_dim
+    sd = {"patch_embed.proj.weight": p["patch_w"].T.reshape(e, 3, 4, 4),
+          "patch_embed.proj.bias": p["patch_b"], "patch_embed.norm.weight": p["pnorm_g"],
+          "patch_embed.norm.bias": p["pnorm_b"], "norm.weight": p["norm_g"],
+          "norm.bias": p["norm_b"], "head.weight": p["head_w"].T, "head.bias": p["head_b"],
+          "layers.0.downsample.norm.weight": p["s1.merge_g"],
+          "layers.0.downsample.norm.bias": p["s1.merge_b"],
+          "layers.0.downsample.reduction.weight": p["s1.merge_w"].T}
+    names = {"norm1.weight": "ln1_g", "norm1.bias": "ln1_b", "attn.qkv.bias": "qkv_b",
+             "attn.relative_position_bias_table": "rpb", "attn.proj.bias": "proj_b",
+             "norm2.weight": "ln2_g", "norm2.bias": "ln2_b", "mlp.fc1.bias": "fc1_b",
+             "mlp.fc2.bias": "fc2_b"}
+    for i in range(2):
+        for j in range(2):
+            src, dst = f"layers.{i}.blocks.{j}.", f"s{i}.b{j}."
+            for a, b in names.items():
+                sd[src + a] = p[dst + b]
+            for a, b in (("attn.qkv.weight", "qkv_w"), ("attn.proj.weight", "proj_w"),
+                         ("mlp.fc1.weight", "fc1_w"), ("mlp.fc2.weight", "fc2_w")):
+                sd[src + a] = p[dst + b].T
+    q = params_from_state_dict(sd, cfg)
+    assert set(q) == set(p)
+    for k in p:
+        assert np.array_equal(q[k], p[k]), k
+
+
+def test_get_swin_names():
+    from edgevisiontransformer_amd.modeling.models.swin import swin_config_from_name
+    c = swin_config_from_name("swin_base_patch4_window7_224")
+    assert c.embed_dim == 128 and c.depths == (2, 2, 18, 2) and c.num_heads == (4, 8, 16, 32)
+    with pytest.raises(NotImplementedError):
+        swin_config_from_name("vit_base")
