@@ -478,7 +478,11 @@ int validate_swin(const evt_swin_desc* d, SwinGeo* g) {
     if (d->num_heads[i] <= 0 || C % d->num_heads[i] || C / d->num_heads[i] != 32)
       return fail(EVT_EINVAL, "head size (stage width / num_heads) must be 32 in this build");
     g->C[i] = C;
-    g->Cst[i] = (int)round_up(C, PAD_N);
+    // Row stride = C (a multiple of 32): no stream padding. The GEMMs that consume these rows
+    // read K rounded up to 64 columns; the columns past C belong to the next row (finite values,
+    // multiplied by the zero-padded weight rows) and the last row's overrun lands in the zeroed
+    // slack SWIN_SLACK at the end of each such buffer.
+    g->Cst[i] = C;
     g->R[i] = R;
     g->mlp[i] = (int)(C * d->mlp_ratio);
     if (g->mlp[i] <= 0) return fail(EVT_EINVAL, "mlp width must be positive");
@@ -486,6 +490,8 @@ int validate_swin(const evt_swin_desc* d, SwinGeo* g) {
   }
   return EVT_OK;
 }
+
+constexpr size_t SWIN_SLACK = 64;  // zeroed elements after x / xm / o (K-padding overrun)
 
 struct SwinWs {  // element / float counts of the Swin workspace for B images
   size_t stream = 0, stats = 0, qkv = 0, o = 0, hbuf = 0, pooled = 0;
@@ -510,7 +516,8 @@ SwinWs swin_ws(const SwinGeo& g, int B) {
 size_t swin_workspace_bytes(const evt_swin_desc* d, const SwinGeo& g, int B) {
   const SwinWs w = swin_ws(g, B);
   const size_t es = elem_size(d->dtype);
-  return (2 * w.stream + w.qkv + w.o + w.hbuf + w.pooled) * es + 2 * w.stats * sizeof(float);
+  return (2 * w.stream + w.qkv + w.o + w.hbuf + w.pooled + 3 * SWIN_SLACK) * es +
+         2 * w.stats * sizeof(float);
 }
 
 }  // namespace
@@ -894,12 +901,15 @@ int evt_swin_create(const evt_swin_desc* desc, const float* const* w, int n_weig
     const int B = desc->max_batch;
     const SwinWs ws = swin_ws(g, B);
     const size_t es = elem_size(desc->dtype);
-    EVT_RC(dev_alloc(m, &m->x, ws.stream * es));
-    EVT_RC(dev_alloc(m, &m->xm, ws.stream * es));
+    EVT_RC(dev_alloc(m, &m->x, (ws.stream + SWIN_SLACK) * es));
+    EVT_RC(dev_alloc(m, &m->xm, (ws.stream + SWIN_SLACK) * es));
+    EVT_HIP(hipMemsetAsync(m->x, 0, (ws.stream + SWIN_SLACK) * es, s), "memset x");
+    EVT_HIP(hipMemsetAsync(m->xm, 0, (ws.stream + SWIN_SLACK) * es, s), "memset xm");
     EVT_RC(dev_alloc(m, (void**)&m->sx, ws.stats * sizeof(float)));
     EVT_RC(dev_alloc(m, (void**)&m->sm, ws.stats * sizeof(float)));
     EVT_RC(dev_alloc(m, &m->qkv, ws.qkv * es));
-    EVT_RC(dev_alloc(m, &m->o, ws.o * es));
+    EVT_RC(dev_alloc(m, &m->o, (ws.o + SWIN_SLACK) * es));
+    EVT_HIP(hipMemsetAsync(m->o, 0, (ws.o + SWIN_SLACK) * es, s), "memset o");
     EVT_RC(dev_alloc(m, &m->hbuf, ws.hbuf * es));
     EVT_RC(dev_alloc(m, &m->pooled, ws.pooled * es));
     if (desc->dtype == DT_BF16) {

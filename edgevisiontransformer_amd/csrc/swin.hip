@@ -31,83 +31,121 @@ namespace {
 constexpr float kLog2e = 1.4426950408889634f;
 
 // ---- patch embedding im2col ----------------------------------------------------------------
+// One block per (patch row py, image b): the [C][ps][S] fp32 strip of the image is staged in LDS
+// with coalesced 16-B loads, then the S/ps output rows (c, kh, kw) leave as 16-B chunks of 8
+// (coalesced row-contiguous stores), zero padded to ldo.
 template <typename TO>
-__global__ __launch_bounds__(256) void swin_patch_kernel(const float* __restrict__ img, int B,
-                                                         int C, int S, int ps,
-                                                         TO* __restrict__ out, int ldo) {
-  const int np = S / ps, pd = C * ps * ps;
-  const int64_t total = (int64_t)B * np * np * ldo;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * 256) {
-    const int64_t row = e / ldo;
-    const int f = (int)(e - row * ldo);
-    float v = 0.f;
-    if (f < pd) {
-      const int b = (int)(row / (np * np)), t = (int)(row - (int64_t)b * np * np);
-      const int py = t / np, px = t - py * np;
-      const int c = f / (ps * ps), r = f - c * ps * ps, kh = r / ps, kw = r - kh * ps;
-      v = img[(((int64_t)b * C + c) * S + py * ps + kh) * S + px * ps + kw];
+__global__ __launch_bounds__(256) void swin_patch_kernel(const float* __restrict__ img, int C,
+                                                         int S, int ps, TO* __restrict__ out,
+                                                         int ldo) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* strip = (float*)smem;
+  const int py = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int np = S / ps, per_c = ps * S, pd = C * ps * ps;
+  for (int c = 0; c < C; ++c) {
+    const float* src = img + (((int64_t)b * C + c) * S + (int64_t)py * ps) * S;
+    for (int i = tid * 4; i < per_c; i += 256 * 4) *(f32x4*)(strip + c * per_c + i) = load4(src + i);
+  }
+  __syncthreads();
+  TO* orow = out + ((int64_t)b * np + py) * np * ldo;
+  const int cpr = ldo / 8;  // 8-element chunks per output row
+  for (int e = tid; e < np * cpr; e += 256) {
+    const int px = e / cpr, f0 = (e - px * cpr) * 8;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int f = f0 + j;
+      v[j] = 0.f;
+      if (f < pd) {
+        const int c = f / (ps * ps), r = f - c * ps * ps, kh = r / ps, kw = r - kh * ps;
+        v[j] = strip[c * per_c + kh * S + px * ps + kw];
+      }
     }
-    out[e] = from_f32<TO>(v);
+    TO* op = orow + (int64_t)px * ldo + f0;
+    store4(op, f32x4{v[0], v[1], v[2], v[3]});
+    store4(op + 4, f32x4{v[4], v[5], v[6], v[7]});
   }
 }
 
 // ---- LayerNorm rows (act dtype in / out) + statistics of the stored output -----------------
-template <typename T, int NV>
+// LPR lanes per row (power of 2 <= 64), each lane NC 16-B chunks (ld <= LPR * NC * V); 64 / LPR
+// rows per wave; reductions over the row's lanes with xor shuffles.
+template <typename T, int LPR, int NC>
 __global__ __launch_bounds__(256) void ln_rows_kernel(const T* __restrict__ x, int64_t ld,
                                                       T* __restrict__ y,
                                                       const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, int rows,
                                                       int D, float eps,
                                                       float* __restrict__ stats, int nslots) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const T* xr = x + (int64_t)row * ld;
-  float v[NV];
+  constexpr int V = 16 / sizeof(T);
+  const int lane = threadIdx.x & 63, sub = lane % LPR;
+  const int row = (blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 / LPR) + lane / LPR;
+  const bool live = row < rows;
+  const T* xr = x + (int64_t)min(row, rows - 1) * ld;
+  float v[NC][V];
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = i * 64 + lane;
-    v[i] = c < D ? to_f32(xr[c]) : 0.f;
-    s += v[i];
+  for (int i = 0; i < NC; ++i) {
+    const int c0 = (i * LPR + sub) * V;
+    u32x4 raw = u32x4{0u, 0u, 0u, 0u};
+    if (c0 < ld) raw = *(const u32x4*)(xr + c0);
+    const T* tv = (const T*)&raw;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      v[i][j] = (c0 + j < D) ? to_f32(tv[j]) : 0.f;
+      s += v[i][j];
+    }
   }
+#pragma unroll
+  for (int o = 1; o < LPR; o <<= 1) s += __shfl_xor(s, o, 64);
   const float inv_d = 1.0f / (float)D;
-  const float mean = wave_sum(s) * inv_d;
+  const float mean = s * inv_d;
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = i * 64 + lane;
-    if (c < D) q += (v[i] - mean) * (v[i] - mean);
-  }
-  const float rstd = rsqrtf(wave_sum(q) * inv_d + eps);
+  for (int i = 0; i < NC; ++i)
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int c = (i * LPR + sub) * V + j;
+      if (c < D) q += (v[i][j] - mean) * (v[i][j] - mean);
+    }
+#pragma unroll
+  for (int o = 1; o < LPR; o <<= 1) q += __shfl_xor(q, o, 64);
+  const float rstd = rsqrtf(q * inv_d + eps);
   T* yr = y + (int64_t)row * ld;
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = i * 64 + lane;
-    if (c < ld) {
-      const T o = from_f32<T>(c < D ? (v[i] - mean) * rstd * gamma[c] + beta[c] : 0.f);
-      yr[c] = o;
-      const float f = to_f32(o);
+  for (int i = 0; i < NC; ++i) {
+    const int c0 = (i * LPR + sub) * V;
+    if (c0 >= ld) continue;
+    T o[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int c = c0 + j;
+      o[j] = from_f32<T>(c < D ? (v[i][j] - mean) * rstd * gamma[c] + beta[c] : 0.f);
+      const float f = to_f32(o[j]);
       s1 += f;
       s2 += f * f;
     }
+    if (live) *(u32x4*)(yr + c0) = *(const u32x4*)o;
   }
-  s1 = wave_sum(s1);
-  s2 = wave_sum(s2);
-  if (lane < nslots) {
-    float* st = stats + 2 * ((int64_t)nslots * row + lane);
-    st[0] = lane == 0 ? s1 : 0.f;
-    st[1] = lane == 0 ? s2 : 0.f;
+#pragma unroll
+  for (int o = 1; o < LPR; o <<= 1) {
+    s1 += __shfl_xor(s1, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+  }
+  if (live && sub < nslots) {
+    float* st = stats + 2 * ((int64_t)nslots * row + sub);
+    st[0] = sub == 0 ? s1 : 0.f;
+    st[1] = sub == 0 ? s2 : 0.f;
   }
 }
 
-// ---- PatchMerging gather: one wave per output row ------------------------------------------
+// ---- PatchMerging gather: one wave per output row, 16-B chunks (C % 8 == 0) -----------------
 template <typename T>
 __global__ __launch_bounds__(256) void merge_kernel(const T* __restrict__ x, int64_t ldx, int B,
                                                     int R, int C, T* __restrict__ out,
                                                     float* __restrict__ stats, int nslots) {
+  constexpr int V = 16 / sizeof(T);  // elements per 16-B chunk
   const int lane = threadIdx.x & 63;
   const int64_t orow = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int R2 = R / 2;
@@ -115,16 +153,21 @@ __global__ __launch_bounds__(256) void merge_kernel(const T* __restrict__ x, int
   const int b = (int)(orow / (R2 * R2)), t = (int)(orow - (int64_t)b * R2 * R2);
   const int oy = t / R2, ox = t - oy * R2;
   T* op = out + orow * 4 * C;
+  const int cq = C / V;  // chunks per quadrant
   float s1 = 0.f, s2 = 0.f;
   // quadrant q: (dy, dx) = (q & 1, q >> 1) (reference order x0, x1, x2, x3)
-  for (int e = lane; e < 4 * C; e += 64) {
-    const int q = e / C, c = e - q * C;
+  for (int e = lane; e < 4 * cq; e += 64) {
+    const int q = e / cq, c = (e - q * cq) * V;
     const int y = 2 * oy + (q & 1), xx = 2 * ox + (q >> 1);
-    const T v = x[((int64_t)b * R * R + (int64_t)y * R + xx) * ldx + c];
-    op[e] = v;
-    const float f = to_f32(v);
-    s1 += f;
-    s2 += f * f;
+    const u32x4 v = *(const u32x4*)(x + ((int64_t)b * R * R + (int64_t)y * R + xx) * ldx + c);
+    *(u32x4*)(op + q * C + c) = v;
+    const T* tv = (const T*)&v;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const float f = to_f32(tv[j]);
+      s1 += f;
+      s2 += f * f;
+    }
   }
   s1 = wave_sum(s1);
   s2 = wave_sum(s2);
@@ -391,23 +434,29 @@ __global__ __launch_bounds__(256) void ln_pool_kernel(const T* __restrict__ x, i
   }
 }
 
+template <typename T, int LPR, int NC>
+hipError_t ln_rows_lc(const void* x, int64_t ld, void* y, const float* g, const float* bb,
+                      int rows, int D, float eps, float* stats, int nslots, hipStream_t s) {
+  const int rows_per_block = 4 * (64 / LPR);
+  hipLaunchKernelGGL((ln_rows_kernel<T, LPR, NC>), dim3((rows + rows_per_block - 1) / rows_per_block),
+                     dim3(256), 0, s, (const T*)x, ld, (T*)y, g, bb, rows, D, eps, stats, nslots);
+  return hipGetLastError();
+}
+
 template <typename T>
 hipError_t ln_rows_t(const void* x, int64_t ld, void* y, const float* g, const float* bb, int rows,
                      int D, float eps, float* stats, int nslots, hipStream_t s) {
-  const dim3 grid((rows + 3) / 4);
-  if (ld <= 128)
-    hipLaunchKernelGGL((ln_rows_kernel<T, 2>), grid, dim3(256), 0, s, (const T*)x, ld, (T*)y, g,
-                       bb, rows, D, eps, stats, nslots);
-  else if (ld <= 256)
-    hipLaunchKernelGGL((ln_rows_kernel<T, 4>), grid, dim3(256), 0, s, (const T*)x, ld, (T*)y, g,
-                       bb, rows, D, eps, stats, nslots);
-  else if (ld <= 512)
-    hipLaunchKernelGGL((ln_rows_kernel<T, 8>), grid, dim3(256), 0, s, (const T*)x, ld, (T*)y, g,
-                       bb, rows, D, eps, stats, nslots);
-  else
-    hipLaunchKernelGGL((ln_rows_kernel<T, 16>), grid, dim3(256), 0, s, (const T*)x, ld, (T*)y, g,
-                       bb, rows, D, eps, stats, nslots);
-  return hipGetLastError();
+  constexpr int V = 16 / sizeof(T);
+  // lanes per row: enough to cover the row in <= 4 chunks each, and >= nslots (slot writers)
+  if (ld <= 8 * V && nslots <= 8)
+    return ln_rows_lc<T, 8, 1>(x, ld, y, g, bb, rows, D, eps, stats, nslots, s);
+  if (ld <= 16 * V && nslots <= 16)
+    return ln_rows_lc<T, 16, 1>(x, ld, y, g, bb, rows, D, eps, stats, nslots, s);
+  if (ld <= 32 * V)
+    return ln_rows_lc<T, 32, 1>(x, ld, y, g, bb, rows, D, eps, stats, nslots, s);
+  if (ld <= 64 * V) return ln_rows_lc<T, 64, 1>(x, ld, y, g, bb, rows, D, eps, stats, nslots, s);
+  if (ld <= 128 * V) return ln_rows_lc<T, 64, 2>(x, ld, y, g, bb, rows, D, eps, stats, nslots, s);
+  return ln_rows_lc<T, 64, 4>(x, ld, y, g, bb, rows, D, eps, stats, nslots, s);
 }
 
 }  // namespace
@@ -415,14 +464,15 @@ hipError_t ln_rows_t(const void* x, int64_t ld, void* y, const float* g, const f
 hipError_t swin_patch_launch(int dtype, const float* img, int B, int C, int S, int ps, void* out,
                              int ldo, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  if (S % ps || C * ps * ps > ldo) return hipErrorInvalidValue;
-  const int64_t total = (int64_t)B * (S / ps) * (S / ps) * ldo;
-  const int grid = (int)std::min<int64_t>((total + 255) / 256, 65536);
+  if (S % ps || C * ps * ps > ldo || ldo % 8 || (ps * S) % 4) return hipErrorInvalidValue;
+  const size_t lds = (size_t)C * ps * S * sizeof(float);
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  const dim3 grid(S / ps, B);
   if (dtype == DT_BF16)
-    hipLaunchKernelGGL(swin_patch_kernel<bf16>, dim3(grid), dim3(256), 0, s, img, B, C, S, ps,
+    hipLaunchKernelGGL(swin_patch_kernel<bf16>, grid, dim3(256), lds, s, img, C, S, ps,
                        (bf16*)out, ldo);
   else
-    hipLaunchKernelGGL(swin_patch_kernel<float>, dim3(grid), dim3(256), 0, s, img, B, C, S, ps,
+    hipLaunchKernelGGL(swin_patch_kernel<float>, grid, dim3(256), lds, s, img, C, S, ps,
                        (float*)out, ldo);
   return hipGetLastError();
 }
@@ -431,7 +481,8 @@ hipError_t ln_rows_launch(int dtype, const void* x, int64_t ld, void* y, const f
                           const float* beta, int rows, int D, float eps, float* stats, int nslots,
                           hipStream_t s) {
   if (rows <= 0) return hipSuccess;
-  if (D <= 0 || D > ld || ld > 1024 || nslots > 64) return hipErrorInvalidValue;
+  if (D <= 0 || D > ld || ld > 1024 || nslots > 64 || ld % (dtype == DT_BF16 ? 8 : 4))
+    return hipErrorInvalidValue;
   return dtype == DT_BF16 ? ln_rows_t<bf16>(x, ld, y, gamma, beta, rows, D, eps, stats, nslots, s)
                           : ln_rows_t<float>(x, ld, y, gamma, beta, rows, D, eps, stats, nslots, s);
 }
@@ -439,7 +490,7 @@ hipError_t ln_rows_launch(int dtype, const void* x, int64_t ld, void* y, const f
 hipError_t merge_launch(int dtype, const void* x, int64_t ldx, int B, int R, int C, void* out,
                         float* stats, int nslots, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  if (R % 2 || C <= 0 || C > ldx || nslots > 64) return hipErrorInvalidValue;
+  if (R % 2 || C <= 0 || C > ldx || nslots > 64 || C % 8 || ldx % 8) return hipErrorInvalidValue;
   const int64_t rows = (int64_t)B * (R / 2) * (R / 2);
   const dim3 grid((unsigned)((rows + 3) / 4));
   if (dtype == DT_BF16)
