@@ -29,149 +29,181 @@ namespace evt {
 
 namespace {
 
-template <int NKT>  // 16-key tiles (keys padded to NKT*16; odd NKT: a half last PV step)
-__global__ __launch_bounds__(256, NKT == 13 ? 3 : 1) void attn_bf16_kernel(AttnParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int NP = NKT * 16;
-  constexpr int ROWB = 128;  // 64 bf16
-  EVT_LDS char* Ks = (EVT_LDS char*)smem;
-  EVT_LDS char* Vs = Ks + NP * ROWB;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.x / p.H, h = blockIdx.x - b * p.H;
-  const bf16* qkv = (const bf16*)p.qkv + (int64_t)b * p.N * p.ldq;
+// One 16-query tile of one (image, head): S^T = K Q^T, softmax, O^T = V^T P^T, stores.
+// Ks / Vs: the head's K and V rows staged in LDS (NKT*16 rows of 128 B, swizzle chunk ^ (row & 7)).
+template <int NKT, bool PLAIN_STORE>
+__device__ __forceinline__ void attn_tile_bf16(const AttnParams& p, const EVT_LDS char* Ks,
+                                               const EVT_LDS char* Vs, u32x4 qf0, u32x4 qf1,
+                                               int qt, int b, int h, int lane) {
+  constexpr int ROWB = 128;
   const int g = lane >> 4, c16 = lane & 15, sw = lane & 7;
-  const int nqt = (p.N + 15) >> 4;
+  f32x4 s[NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    const EVT_LDS char* kr = Ks + (kt * 16 + c16) * ROWB;
+    const u32x4 k0 = *(const EVT_LDS u32x4*)(kr + ((g ^ sw) * 16));
+    const u32x4 k1 = *(const EVT_LDS u32x4*)(kr + (((g + 4) ^ sw) * 16));
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, k0),
+                                                  __builtin_bit_cast(bf16x8, qf0), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, k1),
+                                                  __builtin_bit_cast(bf16x8, qf1), acc, 0, 0, 0);
+    s[kt] = acc;
+  }
+  // s[kt][j] = S^T[key = kt*16 + 4g + j][query = qt*16 + c16]. Keys past N exist only in the
+  // tiles that reach past N (a wave-uniform test): the rest skip the masking VALU work.
+  // (NFULL: tiles that are full for every N this NKT is launched for, attention_launch)
+  constexpr int NFULL = NKT == 13 ? 12 : NKT == 12 ? 8 : NKT == 14 ? 13 : NKT == 16 ? 14 : NKT == 8 ? 4 : 0;
+#pragma unroll
+  for (int kt = NFULL; kt < NKT; ++kt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (kt * 16 + 4 * g + j >= p.N) s[kt][j] = -INFINITY;
+  // scale first (packed multiply): the max then runs on arithmetic results, which the compiler
+  // knows are canonical (fmaxf on raw MFMA results costs a canonicalising v_max per element)
+  const f32x2 sc2 = {p.scale_log2, p.scale_log2};
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      f32x2 v = {s[kt][2 * hh], s[kt][2 * hh + 1]};
+      v = v * sc2;
+      s[kt][2 * hh] = v[0];
+      s[kt][2 * hh + 1] = v[1];
+    }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+    mx = fmaxf(fmaxf(mx, fmaxf(s[kt][0], s[kt][1])), fmaxf(s[kt][2], s[kt][3]));
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  // exp2(s - max) on packed fp32 pairs (v_pk_add_f32)
+  const f32x2 mo2 = {-mx, -mx};
+  f32x2 sum2 = {0.f, 0.f};
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      f32x2 v = {s[kt][2 * hh], s[kt][2 * hh + 1]};
+      v = v + mo2;
+      v[0] = __builtin_amdgcn_exp2f(v[0]);
+      v[1] = __builtin_amdgcn_exp2f(v[1]);
+      s[kt][2 * hh] = v[0];
+      s[kt][2 * hh + 1] = v[1];
+      sum2 += v;
+    }
+  float sum = sum2[0] + sum2[1];
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
 
-  // ---- Q fragments of all this wave's query tiles (wave, wave+4, ...), issued together with
-  // the K/V staging so that every load latency overlaps (NQW = max tiles per wave)
-  constexpr int NQW = (NP / 16 + 3) / 4;
-  u32x4 qf[NQW][2];
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // transposed-read addressing: lane 16g + 4q + pp reads row 4g+q, cols dt*16 + 4pp .. +3
+  const int tq = (lane >> 2) & 3, tp = lane & 3;
+#pragma unroll
+  for (int ks = 0; ks < NKT / 2; ++ks) {
+    bf16x8 pf;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pf[j] = (bf16)s[2 * ks][j];
+      pf[4 + j] = (bf16)s[2 * ks + 1][j];
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep each step's tr-reads next to their MFMAs
+    const int key0 = ks * 32 + 4 * g + tq;  // key0 & 7 == key1 & 7
+    const int ksw = key0 & 7;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int chunk = 2 * dt + (tp >> 1);
+      const int off = ((chunk ^ ksw) * 16) + (tp & 1) * 8;
+      const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((EVT_LDS i16x4*)(Vs + key0 * ROWB + off));
+      const i16x4 v1 =
+          __builtin_amdgcn_ds_read_tr16_b64_v4i16((EVT_LDS i16x4*)(Vs + (key0 + 16) * ROWB + off));
+      const i16x8 vv = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[dt],
+                                                      0, 0, 0);
+    }
+  }
+  if constexpr (NKT % 2) {  // last 16 keys: the upper k half of the MFMA is zero
+    bf16x8 pf;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pf[j] = (bf16)s[NKT - 1][j];
+      pf[4 + j] = (bf16)0.f;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const int key0 = (NKT - 1) * 16 + 4 * g + tq;
+    const int ksw = key0 & 7;
+    const i16x4 z = {0, 0, 0, 0};
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int chunk = 2 * dt + (tp >> 1);
+      const int off = ((chunk ^ ksw) * 16) + (tp & 1) * 8;
+      const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((EVT_LDS i16x4*)(Vs + key0 * ROWB + off));
+      const i16x8 vv = __builtin_shufflevector(v0, z, 0, 1, 2, 3, 4, 5, 6, 7);
+      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[dt],
+                                                      0, 0, 0);
+    }
+  }
+  // o[dt][j] = O^T[d = dt*16 + 4g + j][query]
+  const int q = qt * 16 + c16;
+  if (q < p.N) {
+    const float inv = 1.0f / sum;
+    bf16* op = (bf16*)p.out + ((int64_t)b * p.N + q) * p.ldo + h * 64 + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      if (PLAIN_STORE) store4(op + dt * 16, o[dt] * inv);
+      else store4_nt(op + dt * 16, o[dt] * inv);
+    }
+  }
+}
+
+// Stage one (image, head)'s K and V rows (NP rows, clamped past N) into LDS with glds, WAVES
+// waves sharing the rows, and load the Q fragments of query tiles wave, wave + WAVES, ...
+template <int NKT, int WAVES, int NQW>
+__device__ __forceinline__ void attn_stage_bf16(const AttnParams& p, EVT_LDS char* Ks,
+                                                EVT_LDS char* Vs, u32x4 (&qf)[NQW][2], int b,
+                                                int h, int wave, int lane) {
+  constexpr int NP = NKT * 16, ROWB = 128;
+  const bf16* qkv = (const bf16*)p.qkv + (int64_t)b * p.N * p.ldq;
+  const int g = lane >> 4, c16 = lane & 15;
 #pragma unroll
   for (int i = 0; i < NQW; ++i) {
-    const int qi = min((wave + 4 * i) * 16 + c16, p.N - 1);
+    const int qi = min((wave + WAVES * i) * 16 + c16, p.N - 1);
     const bf16* qrow = qkv + (int64_t)qi * p.ldq + h * 64;
     qf[i][0] = *(const u32x4*)(qrow + 8 * g);
     qf[i][1] = *(const u32x4*)(qrow + 8 * (g + 4));
   }
-  // ---- stage K, V (8 rows of 128 B per wave-instruction) ----
-  {
-    const int srow = lane >> 3, sslot = lane & 7;
-    for (int i = wave; i < NP / 8; i += 4) {
-      const int row = i * 8 + srow;
-      const int gr = min(row, p.N - 1);
-      const bf16* rp = qkv + (int64_t)gr * p.ldq + ((sslot ^ srow) * 8);
-      glds16(rp + (p.H + h) * 64, Ks + i * 8 * ROWB);
-      glds16(rp + (2 * p.H + h) * 64, Vs + i * 8 * ROWB);
-    }
-    wait_vmcnt0();
-    __syncthreads();
+  const int srow = lane >> 3, sslot = lane & 7;  // 8 rows of 128 B per wave-instruction
+  for (int i = wave; i < NP / 8; i += WAVES) {
+    const int row = i * 8 + srow;
+    const int gr = min(row, p.N - 1);
+    const bf16* rp = qkv + (int64_t)gr * p.ldq + ((sslot ^ srow) * 8);
+    glds16(rp + (p.H + h) * 64, Ks + i * 8 * ROWB);
+    glds16(rp + (2 * p.H + h) * 64, Vs + i * 8 * ROWB);
   }
+}
 
+// One workgroup (4 waves) per (image, head); 3 per CU (53 KiB of LDS each).
+template <int NKT>  // 16-key tiles (keys padded to NKT*16; odd NKT: a half last PV step)
+__global__ __launch_bounds__(256, (NKT == 13 || NKT == 12) ? 3 : 1) void attn_bf16_kernel(AttnParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NP = NKT * 16, ROWB = 128;
+  constexpr int NQW = (NP / 16 + 3) / 4;
+  EVT_LDS char* Ks = (EVT_LDS char*)smem;
+  EVT_LDS char* Vs = Ks + NP * ROWB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x / p.H, h = blockIdx.x - b * p.H;
+  const int nqt = (p.N + 15) >> 4;
+  u32x4 qf[NQW][2];
+  attn_stage_bf16<NKT, 4, NQW>(p, Ks, Vs, qf, b, h, wave, lane);
+  wait_vmcnt0();
+  __syncthreads();
 #pragma unroll
   for (int it = 0; it < NQW; ++it) {
     const int qt = wave + 4 * it;
     if (qt >= nqt) break;
-    const u32x4 qf0 = qf[it][0];
-    const u32x4 qf1 = qf[it][1];
-
-    f32x4 s[NKT];
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
-      const EVT_LDS char* kr = Ks + (kt * 16 + c16) * ROWB;
-      const u32x4 k0 = *(const EVT_LDS u32x4*)(kr + ((g ^ sw) * 16));
-      const u32x4 k1 = *(const EVT_LDS u32x4*)(kr + (((g + 4) ^ sw) * 16));
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, k0),
-                                                    __builtin_bit_cast(bf16x8, qf0), acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, k1),
-                                                    __builtin_bit_cast(bf16x8, qf1), acc, 0, 0, 0);
-      s[kt] = acc;
-    }
-    // s[kt][j] = S^T[key = kt*16 + 4g + j][query = qt*16 + c16]
-    float mx = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int key = kt * 16 + 4 * g + j;
-        if (key >= p.N) s[kt][j] = -INFINITY;
-        mx = fmaxf(mx, s[kt][j]);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float moff = mx * p.scale_log2;
-    float sum = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float e = __builtin_amdgcn_exp2f(s[kt][j] * p.scale_log2 - moff);
-        s[kt][j] = e;
-        sum += e;
-      }
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
-
-    f32x4 o[4];
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // transposed-read addressing: lane 16g + 4q + pp reads row 4g+q, cols dt*16 + 4pp .. +3
-    const int tq = (lane >> 2) & 3, tp = lane & 3;
-#pragma unroll
-    for (int ks = 0; ks < NKT / 2; ++ks) {
-      bf16x8 pf;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        pf[j] = (bf16)s[2 * ks][j];
-        pf[4 + j] = (bf16)s[2 * ks + 1][j];
-      }
-      __builtin_amdgcn_sched_barrier(0);  // keep each step's tr-reads next to their MFMAs
-      const int key0 = ks * 32 + 4 * g + tq;  // key0 & 7 == key1 & 7
-      const int ksw = key0 & 7;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int chunk = 2 * dt + (tp >> 1);
-        const int off = ((chunk ^ ksw) * 16) + (tp & 1) * 8;
-        const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (EVT_LDS i16x4*)(Vs + key0 * ROWB + off));
-        const i16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (EVT_LDS i16x4*)(Vs + (key0 + 16) * ROWB + off));
-        const i16x8 vv = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[dt],
-                                                        0, 0, 0);
-      }
-    }
-    if constexpr (NKT % 2) {  // last 16 keys: the upper k half of the MFMA is zero
-      bf16x8 pf;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        pf[j] = (bf16)s[NKT - 1][j];
-        pf[4 + j] = (bf16)0.f;
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      const int key0 = (NKT - 1) * 16 + 4 * g + tq;
-      const int ksw = key0 & 7;
-      const i16x4 z = {0, 0, 0, 0};
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int chunk = 2 * dt + (tp >> 1);
-        const int off = ((chunk ^ ksw) * 16) + (tp & 1) * 8;
-        const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (EVT_LDS i16x4*)(Vs + key0 * ROWB + off));
-        const i16x8 vv = __builtin_shufflevector(v0, z, 0, 1, 2, 3, 4, 5, 6, 7);
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[dt],
-                                                        0, 0, 0);
-      }
-    }
-    // o[dt][j] = O^T[d = dt*16 + 4g + j][query]
-    const int q = qt * 16 + c16;
-    if (q < p.N) {
-      const float inv = 1.0f / sum;
-      bf16* op = (bf16*)p.out + ((int64_t)b * p.N + q) * p.ldo + h * 64 + 4 * g;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) store4_nt(op + dt * 16, o[dt] * inv);
-    }
+    attn_tile_bf16<NKT, true>(p, Ks, Vs, qf[it][0], qf[it][1], qt, b, h, lane);
   }
 }
 
@@ -307,8 +339,9 @@ hipError_t attention_launch(int dtype, const AttnParams& p, hipStream_t s) {
   set_lds_attrs();
   if (p.N <= 64) return launch_nkt<4>(dtype, p, s);
   if (p.N <= 128) return launch_nkt<8>(dtype, p, s);
+  if (dtype == DT_BF16 && p.N <= 192) return launch_nkt<12>(dtype, p, s);
   if (dtype == DT_BF16 && p.N <= 208) return launch_nkt<13>(dtype, p, s);  // 3 blocks per CU (LDS)
-  if (p.N <= 224) return launch_nkt<14>(dtype, p, s);
+  if (p.N <= 224) return launch_nkt<14>(dtype, p, s);  // (f32: N in (128, 224])
   return launch_nkt<16>(dtype, p, s);
 }
 
