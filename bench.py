@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-probe", action="store_true", help="skip the per-kernel probe")
+    ap.add_argument("--gemm-variant", type=int, default=0, help="evt_set_gemm_variant (tuning A/B)")
     ap.add_argument("--probe-only", type=int, default=0, metavar="N",
                     help="only launch the FC1 probe kernel N times and exit (PMC collection)")
     return ap.parse_args()
@@ -186,6 +187,9 @@ def main():
     else:
         from edgevisiontransformer_amd.modeling.models import vit as mod
     model = mod.build_named(args.model, dtype=args.dtype, seed=0, max_batch=args.batch)
+    if args.gemm_variant:
+        from edgevisiontransformer_amd import _lib
+        _lib.check(_lib.load_library().evt_set_gemm_variant(args.gemm_variant))
     B = args.batch
     g = torch.Generator(device="cuda").manual_seed(1000 + rank)
     shape = (B, 224, 224, 3) if t2t else (B, 3, 224, 224)   # T2T-ViT is channel-last

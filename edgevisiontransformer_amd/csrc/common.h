@@ -69,6 +69,40 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return x * (x >= 0.f ? 1.0f - q : q);
 }
 
+// Packed-pair forms of the two GELUs (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 for everything but
+// the transcendentals, which have no packed form): the GEMM epilogues are VALU-bound on these.
+__device__ __forceinline__ f32x2 gelu_tanh2(f32x2 x) {
+  const float c1 = -2.0f * 0.7978845608028654f * 1.4426950408889634f;
+  const float c3 = c1 * 0.044715f;
+  const f32x2 u = x * (f32x2{c1, c1} + f32x2{c3, c3} * (x * x));
+  const f32x2 d = f32x2{1.f, 1.f} + f32x2{__builtin_amdgcn_exp2f(u[0]), __builtin_amdgcn_exp2f(u[1])};
+  return x * f32x2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+}
+// A&S 7.1.26 as in gelu_erf, rescaled so that z' = |x| sqrt(log2 e / 2): exp(-x^2/2) = 2^(-z'^2),
+// t = 1 / (1 + p' z') with p' = 0.3275911 / sqrt(log2 e), polynomial coefficients pre-halved (the
+// 0.5 of 0.5 erfc), Phi = 0.5 + copysign(0.5 - q, x).
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
+  const float cz = 0.7071067811865476f * 1.2011224087864498f;  // sqrt(1/2) * sqrt(log2 e)
+  const float pp = 0.3275911f / 1.2011224087864498f;
+  const f32x2 z = f32x2{fabsf(x[0]), fabsf(x[1])} * f32x2{cz, cz};
+  const f32x2 d = f32x2{1.f, 1.f} + f32x2{pp, pp} * z;
+  const f32x2 t = f32x2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  const f32x2 a5 = {0.5f * 1.061405429f, 0.5f * 1.061405429f}, a4 = {0.5f * -1.453152027f, 0.5f * -1.453152027f};
+  const f32x2 a3 = {0.5f * 1.421413741f, 0.5f * 1.421413741f}, a2 = {0.5f * -0.284496736f, 0.5f * -0.284496736f};
+  const f32x2 a1 = {0.5f * 0.254829592f, 0.5f * 0.254829592f};
+  const f32x2 p = t * (a1 + t * (a2 + t * (a3 + t * (a4 + t * a5))));
+  const f32x2 zz = z * z;
+  const f32x2 q = p * f32x2{__builtin_amdgcn_exp2f(-zz[0]), __builtin_amdgcn_exp2f(-zz[1])};
+  const f32x2 h = f32x2{0.5f, 0.5f} - q;
+  const f32x2 phi = f32x2{0.5f, 0.5f} + f32x2{copysignf(h[0], x[0]), copysignf(h[1], x[1])};
+  return x * phi;
+}
+__device__ __forceinline__ f32x4 gelu4(f32x4 v, bool erf_form) {
+  const f32x2 lo = erf_form ? gelu_erf2(f32x2{v[0], v[1]}) : gelu_tanh2(f32x2{v[0], v[1]});
+  const f32x2 hi = erf_form ? gelu_erf2(f32x2{v[2], v[3]}) : gelu_tanh2(f32x2{v[2], v[3]});
+  return f32x4{lo[0], lo[1], hi[0], hi[1]};
+}
+
 // Wave64 reductions (butterfly over all 64 lanes).
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

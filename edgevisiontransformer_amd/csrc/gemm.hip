@@ -161,14 +161,7 @@ __device__ __forceinline__ void epi_rows_t(const GemmParams& p, EVT_LDS char* st
     } else if (FL & EPI_BIAS) {
       v += bias4;
     }
-    if (FL & EPI_GELU) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(v[j]);
-    }
-    if (FL & EPI_GELU_ERF) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = gelu_erf(v[j]);
-    }
+    if (FL & (EPI_GELU | EPI_GELU_ERF)) v = gelu4(v, (FL & EPI_GELU_ERF) != 0);
     if (FL & EPI_POS) {
       const int img = m / p.P, t = m - img * p.P;
       orow = (int64_t)img * (p.P + 1) + 1 + t;
@@ -296,9 +289,7 @@ __device__ __forceinline__ void epi_rows8_t(const GemmParams& p, EVT_LDS char* s
     }
     if (FL & (EPI_GELU | EPI_GELU_ERF)) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[h][j] = (FL & EPI_GELU) ? gelu_tanh(v[h][j]) : gelu_erf(v[h][j]);
+      for (int h = 0; h < 2; ++h) v[h] = gelu4(v[h], (FL & EPI_GELU_ERF) != 0);
     }
     if (FL & EPI_POS) {
       const int img = m / p.P, t = m - img * p.P;
@@ -915,7 +906,10 @@ __device__ __forceinline__ void swap_rows16(f32x4& a, f32x4& b) {
   b = f32x4{y0, y1, y2, y3};
 }
 
-template <int FL, int DBG = 0>
+// PADN: the output width N is not a multiple of the tile (Swin / pruned widths): column groups
+// entirely past N skip their epilogue VALU work. Compiled out otherwise (the check alone cost
+// 2-4 % on the DeiT shapes, measured in one process).
+template <int FL, int DBG = 0, bool PADN = true>
 __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
                                               int wave, int wm, int wn, int m0, int n0, int tn,
                                               int lane, bool interior) {
@@ -942,6 +936,7 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
       }
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
+        if (PADN && !interior && n0 + wn * 64 + nt * 16 >= p.N) continue;  // padding: skip
         if (FL & EPI_LNIN) acc[nt][mt] = acc[nt][mt] * r - c4[nt] * (r * mu) + b4[nt];
         else acc[nt][mt] += b4[nt];
       }
@@ -949,12 +944,12 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
   }
   if constexpr ((FL & (EPI_GELU | EPI_GELU_ERF)) != 0) {
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
+    for (int nt = 0; nt < 4; ++nt) {
+      // column group past N (padding of the packed width): wave-uniform skip of the VALU work
+      if (PADN && !interior && n0 + wn * 64 + nt * 16 >= p.N) continue;
 #pragma unroll
-      for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[nt][mt][j] = (FL & EPI_GELU) ? gelu_tanh(acc[nt][mt][j]) : gelu_erf(acc[nt][mt][j]);
+      for (int mt = 0; mt < 8; ++mt) acc[nt][mt] = gelu4(acc[nt][mt], (FL & EPI_GELU_ERF) != 0);
+    }
   }
   // 2. store layout: pair (2k, 2k+1) -> lane row wm*128 + (2k + (fg & 1))*16 + frow, columns
   //    wn*64 + nt*16 + (fg >> 1)*8 + [acc[nt][2k][0..3], acc[nt][2k+1][0..3]]
@@ -1091,7 +1086,7 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
   }
 }
 
-template <int FL, int DBG = 0>
+template <int FL, int DBG = 0, bool PADN = true>
 __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int total) {
   __shared__ __attribute__((aligned(16))) char smem[PERS_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1142,7 +1137,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
     __builtin_amdgcn_sched_barrier(0);
     stamp(2);
     const bool interior = (m0 + BIG_BM <= p.M) && (n0 + BIG_BN <= p.N);
-    pers_epilogue<FL, DBG>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior);
+    pers_epilogue<FL, DBG, PADN>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior);
     stamp(3);
     ++iter;
     if (!has_next) break;
@@ -1362,6 +1357,8 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 3>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 15)  // timeline probe + staggered block start
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 5>), dim3(G), dim3(512), 0, s, q, total);
+  else if (p.N % BIG_BN == 0)
+    hipLaunchKernelGGL((gemm_pers_kernel<FL, 0, false>), dim3(G), dim3(512), 0, s, q, total);
   else
     hipLaunchKernelGGL((gemm_pers_kernel<FL>), dim3(G), dim3(512), 0, s, q, total);
   return hipGetLastError();
