@@ -33,18 +33,26 @@ import numpy as np
 
 VIT_NAMED = {"deit_tiny": 3, "deit_small": 6, "deit_base": 12}   # heads (vit.py:100-109)
 T2T_NAMED = ("t2t_vit_7", "t2t_vit_10", "t2t_vit_12", "t2t_vit_14")
+SWIN_NAMED = ("swin_tiny", "swin_small", "swin_base")   # get_swin configs (tools.py:282)
 
 
 def build_model(name: str, compute_dtype: str, prune_encoding: Optional[str] = None,
                 max_batch: int = 1, seed: int = 0):
-    """A model by reference name (deit_*, t2t_vit_*), optionally head/FFN pruned."""
+    """A model by reference name (deit_*, t2t_vit_*, swin_*), optionally head/FFN pruned."""
+    if name in SWIN_NAMED or name.startswith("swin_") and name.endswith("_224"):
+        if prune_encoding:
+            raise ValueError("prune_encoding applies to DeiT models only")
+        from .modeling.models.swin import get_swin
+        cfg_name = name if name.endswith("_224") else f"{name}_patch4_window7_224"
+        return get_swin(cfg_name, dtype=compute_dtype, seed=seed, max_batch=max_batch)
     if name in T2T_NAMED:
         if prune_encoding:
             raise ValueError("prune_encoding applies to DeiT models only")
         from .modeling.models.t2t_vit import build_named
         return build_named(name, dtype=compute_dtype, seed=seed, max_batch=max_batch)
     if name not in VIT_NAMED:
-        raise ValueError(f"unknown model {name!r}; one of {sorted(VIT_NAMED) + list(T2T_NAMED)}")
+        raise ValueError(f"unknown model {name!r}; one of "
+                         f"{sorted(VIT_NAMED) + list(T2T_NAMED) + list(SWIN_NAMED)}")
     from .modeling.models.vit import ViT_Pruned, build_named
     if prune_encoding:
         h = VIT_NAMED[name]
