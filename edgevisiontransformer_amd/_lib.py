@@ -42,7 +42,11 @@ class evt_vit_desc(ctypes.Structure):
                 ("heads", ctypes.POINTER(ctypes.c_int32)),
                 ("head_dim", ctypes.POINTER(ctypes.c_int32)),
                 ("ffn", ctypes.POINTER(ctypes.c_int32)),
-                ("dtype", ctypes.c_int32), ("max_batch", ctypes.c_int32)]
+                ("dtype", ctypes.c_int32), ("max_batch", ctypes.c_int32),
+                ("semantics", ctypes.c_int32), ("layer_norm_eps", ctypes.c_float)]
+
+
+VIT_REFERENCE, VIT_STANDARD = 0, 1
 
 
 class evt_dense_args(ctypes.Structure):

@@ -94,7 +94,9 @@ struct SwinStage {
 };
 
 struct evt_model {
-  int family = 0;            // 0: ViT / ViT_Pruned, 1: T2T-ViT
+  int family = 0;            // 0: ViT / ViT_Pruned, 1: T2T-ViT, 2: Swin
+  bool standard = false;     // ViT with EVT_VIT_STANDARD semantics
+  float eps = 1e-5f;         // LayerNorm epsilon of every folded LayerNorm
   int dtype = 0, D = 0, max_batch = 0, num_classes = 0;
   evt_vit_desc desc{};       // ViT only
   evt_t2t_desc tdesc{};      // T2T only
@@ -156,6 +158,9 @@ int validate(const evt_vit_desc* d, Shape* sh) {
   if (d->dim <= 0 || d->dim % 64 != 0 || d->dim > 1024)
     return fail(EVT_EINVAL, "dim must be a positive multiple of 64 and <= 1024");
   if (d->max_batch <= 0) return fail(EVT_EINVAL, "max_batch must be positive");
+  if (d->semantics != EVT_VIT_REFERENCE && d->semantics != EVT_VIT_STANDARD)
+    return fail(EVT_EINVAL, "semantics must be EVT_VIT_REFERENCE or EVT_VIT_STANDARD");
+  if (d->layer_norm_eps < 0.f) return fail(EVT_EINVAL, "layer_norm_eps must be >= 0");
   if (d->depth > 0 && (!d->heads || !d->head_dim || !d->ffn))
     return fail(EVT_EINVAL, "heads/head_dim/ffn arrays are required");
   const int np = d->image_size / d->patch_size;
@@ -275,7 +280,7 @@ int dense(const evt_model* m, const DenseW& w, const DenseCall& c, hipStream_t s
   p.stats_out = c.stats_out;
   const int width = c.ln_width ? c.ln_width : m->D;
   p.inv_d = 1.0f / (float)width;
-  p.eps = 1e-5f;  // Keras LayerNormalization(epsilon=1e-5), reference norm.py:6
+  p.eps = m->eps;  // Keras LayerNormalization(epsilon=1e-5), reference norm.py:6
   p.nslots = stats_slots(c.slot_width ? c.slot_width : width);
   p.stats_step = c.stats_step;
   gemm_sk_bind(m->sk, p);
@@ -284,10 +289,12 @@ int dense(const evt_model* m, const DenseW& w, const DenseCall& c, hipStream_t s
 }
 
 
-// Encoder weights (11 tensors per layer, evt_vit_num_weights order) for m->heads / m->ffn.
+// Encoder weights (11 tensors per layer, 12 with the STANDARD qkv bias; evt_vit_num_weights
+// order) for m->heads / m->ffn.
 int build_encoder(evt_model* m, const float* const* w, hipStream_t s) {
   const int D = m->D;
   const int depth = (int)m->heads.size();
+  const int qb = m->standard ? 1 : 0;  // qkv bias present
   m->layers.resize(depth);
   int k = 0;
   for (int i = 0; i < depth; ++i) {
@@ -298,7 +305,9 @@ int build_encoder(evt_model* m, const float* const* w, hipStream_t s) {
     L.ffn_st = (int)round_up(L.ffn, PAD_N);
     EVT_RC(copy_vec(m, &L.ln1_g, w[k + 0], D, s));
     EVT_RC(copy_vec(m, &L.ln1_b, w[k + 1], D, s));
-    EVT_RC(make_dense(m, &L.qkv, w[k + 2], nullptr, D, 3 * L.inner, s, w[k + 0], w[k + 1]));
+    EVT_RC(make_dense(m, &L.qkv, w[k + 2], qb ? w[k + 3] : nullptr, D, 3 * L.inner, s, w[k + 0],
+                      w[k + 1]));
+    k += qb;
     EVT_RC(make_dense(m, &L.out, w[k + 3], w[k + 4], L.inner, D, s));
     EVT_RC(copy_vec(m, &L.ln2_g, w[k + 5], D, s));
     EVT_RC(copy_vec(m, &L.ln2_b, w[k + 6], D, s));
@@ -343,24 +352,26 @@ int run_encoder(evt_model* m, int B, hipStream_t s) {
     }
     AttnParams ap{m->qkv, 3 * L.inner, m->o, L.inner, T, L.heads, B, 0.125f * log2e};
     EVT_HIP(attention_launch(m->dtype, ap, s), "attention");
-    {  // out-proj + bias + LN1(x) residual -> xm (+ stats)
+    {  // out-proj + bias + LN1(x) residual -> xm (+ stats); STANDARD: + x
       DenseCall c;
-      c.flags = EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS;
+      c.flags = m->standard ? (EPI_BIAS | EPI_RESID | EPI_STATS)
+                            : (EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS);
       c.A = m->o; c.lda = L.inner; c.C = m->xm; c.ldc = D; c.M = rows; c.N = D;
       c.resid = m->x; c.ldr = D; c.rstats = m->sx; c.rgamma = L.ln1_g; c.rbeta = L.ln1_b;
       c.stats_out = m->sm;
       EVT_RC(dense(m, L.out, c, s));
     }
-    {  // LN2-folded FC1 + GELU (ffn.py:8)
+    {  // LN2-folded FC1 + GELU (ffn.py:8; STANDARD: exact erf GELU)
       DenseCall c;
-      c.flags = EPI_LNIN | EPI_BIAS | EPI_GELU;
+      c.flags = EPI_LNIN | EPI_BIAS | (m->standard ? EPI_GELU_ERF : EPI_GELU);
       c.A = m->xm; c.lda = D; c.C = m->hbuf; c.ldc = L.ffn_st; c.M = rows; c.N = L.ffn_st;
       c.stats_in = m->sm;
       EVT_RC(dense(m, L.fc1, c, s));
     }
-    {  // FC2 + bias + LN2(xm) residual -> x (+ stats)
+    {  // FC2 + bias + LN2(xm) residual -> x (+ stats); STANDARD: + xm
       DenseCall c;
-      c.flags = EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS;
+      c.flags = m->standard ? (EPI_BIAS | EPI_RESID | EPI_STATS)
+                            : (EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS);
       c.A = m->hbuf; c.lda = L.ffn_st; c.C = m->x; c.ldc = D; c.M = rows; c.N = D;
       c.resid = m->xm; c.ldr = D; c.rstats = m->sm; c.rgamma = L.ln2_g; c.rbeta = L.ln2_b;
       c.stats_out = m->sx;
@@ -541,7 +552,7 @@ const char* evt_last_error(void) { return g_err.c_str(); }
 
 int evt_vit_num_weights(const evt_vit_desc* desc) {
   if (!desc || desc->depth < 0) return fail(EVT_EINVAL, "bad desc");
-  return 4 + 11 * desc->depth + 4;
+  return 4 + (desc->semantics == EVT_VIT_STANDARD ? 12 : 11) * desc->depth + 4;
 }
 
 int evt_query_workspace(const evt_vit_desc* desc, int batch, size_t* bytes) {
@@ -579,6 +590,8 @@ int evt_vit_create(const evt_vit_desc* desc, const float* const* w, int n_weight
   m->max_batch = desc->max_batch;
   m->num_classes = desc->num_classes;
   m->desc = *desc;
+  m->standard = desc->semantics == EVT_VIT_STANDARD;
+  if (desc->layer_norm_eps > 0.f) m->eps = desc->layer_norm_eps;
   m->heads.assign(desc->heads, desc->heads + desc->depth);
   m->head_dim.assign(desc->head_dim, desc->head_dim + desc->depth);
   m->ffn.assign(desc->ffn, desc->ffn + desc->depth);
@@ -592,9 +605,14 @@ int evt_vit_create(const evt_vit_desc* desc, const float* const* w, int n_weight
     EVT_RC(copy_vec(m, &m->cls, w[2], D, s));
     EVT_RC(copy_vec(m, &m->pos, w[3], (size_t)sh.T * D, s));
     EVT_RC(build_encoder(m, w + 4, s));
-    const int k = 4 + 11 * desc->depth;
-    EVT_RC(make_dense(m, &m->head1, w[k + 0], w[k + 1], D, desc->mlp_dim, s));
-    EVT_RC(make_dense(m, &m->head2, w[k + 2], w[k + 3], desc->mlp_dim, desc->num_classes, s));
+    const int k = 4 + (m->standard ? 12 : 11) * desc->depth;
+    if (m->standard) {  // final LayerNorm folded into the classifier (CLS rows)
+      EVT_RC(make_dense(m, &m->head, w[k + 2], w[k + 3], D, desc->num_classes, s, w[k + 0],
+                        w[k + 1]));
+    } else {
+      EVT_RC(make_dense(m, &m->head1, w[k + 0], w[k + 1], D, desc->mlp_dim, s));
+      EVT_RC(make_dense(m, &m->head2, w[k + 2], w[k + 3], desc->mlp_dim, desc->num_classes, s));
+    }
     const int B = desc->max_batch;
     const size_t es = elem_size(desc->dtype);
     EVT_RC(alloc_encoder_ws(m, B, std::max((size_t)B * sh.T * sh.max_ffn_st,
@@ -629,6 +647,14 @@ int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* 
     EVT_RC(dense(m, m->patch, c, s));
   }
   EVT_RC(run_encoder(m, B, s));
+  if (m->standard) {  // final LayerNorm of the CLS rows folded into the Linear head
+    DenseCall c;
+    c.flags = EPI_LNIN | EPI_BIAS | EPI_OUT_F32;
+    c.A = m->x; c.lda = (int64_t)T * D; c.C = logits; c.ldc = d.num_classes; c.M = B;
+    c.N = d.num_classes; c.stats_in = m->sx; c.stats_step = T;
+    EVT_RC(dense(m, m->head, c, s));
+    return EVT_OK;
+  }
   // head on token 0 (vit.py:54-55; no final LayerNorm): rows b*T of the stream, stride T*D
   {
     DenseCall c;

@@ -25,7 +25,8 @@ import numpy as np
 import torch
 
 from ... import _lib
-from ...weights import ViTConfig, make_vit_params, vit_config, vit_param_shapes
+from ...weights import (ViTConfig, make_std_vit_params, make_vit_params, std_vit_param_shapes,
+                        vit_config, vit_param_shapes)
 
 
 def decode_prune_encoding(prune_encoding: str):
@@ -90,6 +91,11 @@ def _replay_graph(model) -> None:
 class ViT:
     """Vision Transformer forward on MI355X (reference `ViT`, vit.py:9-55)."""
 
+    SEMANTICS = _lib.VIT_REFERENCE
+    _param_shapes = staticmethod(vit_param_shapes)
+    _make_params = staticmethod(make_vit_params)
+    layer_norm_eps = 0.0  # 0: the library default 1e-5 (reference norm.py:6)
+
     def __init__(self, *, image_size=224, patch_size=16, num_classes=1000, dim=768, depth=12,
                  heads=12, mlp_dim=3072, dtype: str = "bf16", seed: int = 0,
                  weights: Optional[Dict[str, np.ndarray]] = None, device=None, max_batch: int = 0,
@@ -109,9 +115,9 @@ class ViT:
         self.device = torch.device(device) if device is not None else torch.device(
             "cuda", torch.cuda.current_device() if torch.cuda.is_available() else 0)
         _lib.ensure_device(self.device.index or 0)
-        params = weights if weights is not None else make_vit_params(self.cfg, seed=seed)
+        params = weights if weights is not None else self._make_params(self.cfg, seed=seed)
         self._weights: List[torch.Tensor] = []
-        for name, shape in vit_param_shapes(self.cfg):
+        for name, shape in self._param_shapes(self.cfg):
             a = np.asarray(params[name], dtype=np.float32)
             if tuple(a.shape) != tuple(shape):
                 if a.size == int(np.prod(shape)) and name == "cls":
@@ -133,7 +139,7 @@ class ViT:
         self._arrays = (heads, hd, ffn)  # keep alive
         return _lib.evt_vit_desc(c.image_size, c.patch_size, c.in_chans, c.num_classes, c.dim,
                                  c.depth, c.mlp_dim, heads, hd, ffn, _lib.DTYPE[self.dtype],
-                                 max_batch)
+                                 max_batch, self.SEMANTICS, self.layer_norm_eps)
 
     def _build(self, max_batch: int) -> None:
         lib = _lib.load_library()
@@ -253,6 +259,86 @@ def pruned_config(prune_encoding: str, *, dim: int, depth: int, heads: int, mlp_
         hl, fl = nh, [int(t * mlp_dim) for t in thr]
     return vit_config(dim, depth, heads, mlp_dim, image_size=image_size, patch_size=patch_size,
                       num_classes=num_classes, head_size=head_size, heads_list=hl, ffn_list=fl)
+
+
+class StandardViT(ViT):
+    """The published DeiT / ViT architecture (timm `VisionTransformer`, HF `ViTForImageClassification`
+    — what the reference evaluates for accuracy via `get_torch_deit`, utils.py:52-62): pre-norm
+    residual x + f(LN(x)), QKV with bias, exact GELU, final LayerNorm, Linear head on the CLS token.
+    Load real checkpoints with `params_from_timm_state_dict` / `params_from_hf_state_dict`."""
+
+    SEMANTICS = _lib.VIT_STANDARD
+    _param_shapes = staticmethod(std_vit_param_shapes)
+    _make_params = staticmethod(make_std_vit_params)
+
+    def __init__(self, *, image_size=224, patch_size=16, num_classes=1000, dim=768, depth=12,
+                 heads=12, mlp_ratio=4.0, layer_norm_eps=1e-6, **kw):
+        self.layer_norm_eps = float(layer_norm_eps)
+        super().__init__(image_size=image_size, patch_size=patch_size, num_classes=num_classes,
+                         dim=dim, depth=depth, heads=heads, mlp_dim=int(dim * mlp_ratio), **kw)
+
+
+def deit_tiny_patch16_224(**kw) -> StandardViT:
+    return StandardViT(dim=192, heads=3, **kw)
+
+
+def deit_small_patch16_224(**kw) -> StandardViT:
+    return StandardViT(dim=384, heads=6, **kw)
+
+
+def deit_base_patch16_224(**kw) -> StandardViT:
+    return StandardViT(dim=768, heads=12, **kw)
+
+
+def _patch_rows(conv_w: np.ndarray) -> np.ndarray:
+    """Conv2d kernel [D, C, p, p] -> patch_w [p*p*C, D] in this build's (p1 p2 c) vector order
+    (the reference's einops pattern, vit.py:31-32)."""
+    d = conv_w.shape[0]
+    return np.ascontiguousarray(conv_w.transpose(2, 3, 1, 0).reshape(-1, d))
+
+
+def params_from_timm_state_dict(sd: Dict[str, np.ndarray], depth: int) -> Dict[str, np.ndarray]:
+    """timm `VisionTransformer` / `deit_*_patch16_224` state dict -> StandardViT parameters."""
+    a = lambda k: np.asarray(sd[k], dtype=np.float32)  # noqa: E731
+    p = {"patch_w": _patch_rows(a("patch_embed.proj.weight")), "patch_b": a("patch_embed.proj.bias"),
+         "cls": a("cls_token").reshape(-1), "pos": a("pos_embed")[0],
+         "norm_g": a("norm.weight"), "norm_b": a("norm.bias"),
+         "head_w": a("head.weight").T, "head_b": a("head.bias")}
+    for i in range(depth):
+        s = f"blocks.{i}."
+        p.update({f"l{i}.ln1_g": a(s + "norm1.weight"), f"l{i}.ln1_b": a(s + "norm1.bias"),
+                  f"l{i}.qkv_w": a(s + "attn.qkv.weight").T, f"l{i}.qkv_b": a(s + "attn.qkv.bias"),
+                  f"l{i}.out_w": a(s + "attn.proj.weight").T, f"l{i}.out_b": a(s + "attn.proj.bias"),
+                  f"l{i}.ln2_g": a(s + "norm2.weight"), f"l{i}.ln2_b": a(s + "norm2.bias"),
+                  f"l{i}.fc1_w": a(s + "mlp.fc1.weight").T, f"l{i}.fc1_b": a(s + "mlp.fc1.bias"),
+                  f"l{i}.fc2_w": a(s + "mlp.fc2.weight").T, f"l{i}.fc2_b": a(s + "mlp.fc2.bias")})
+    return {k: np.ascontiguousarray(v) for k, v in p.items()}
+
+
+def params_from_hf_state_dict(sd: Dict[str, np.ndarray], depth: int) -> Dict[str, np.ndarray]:
+    """HF `ViTForImageClassification` (facebook/deit-*-patch16-224) state dict -> parameters."""
+    a = lambda k: np.asarray(sd[k], dtype=np.float32)  # noqa: E731
+    e = "vit.embeddings."
+    p = {"patch_w": _patch_rows(a(e + "patch_embeddings.projection.weight")),
+         "patch_b": a(e + "patch_embeddings.projection.bias"),
+         "cls": a(e + "cls_token").reshape(-1), "pos": a(e + "position_embeddings")[0],
+         "norm_g": a("vit.layernorm.weight"), "norm_b": a("vit.layernorm.bias"),
+         "head_w": a("classifier.weight").T, "head_b": a("classifier.bias")}
+    for i in range(depth):
+        s = f"vit.layers.{i}."
+        q, k, v = (a(s + f"attention.{n}_proj.weight") for n in "qkv")
+        qb, kb, vb = (a(s + f"attention.{n}_proj.bias") for n in "qkv")
+        p.update({f"l{i}.ln1_g": a(s + "layernorm_before.weight"),
+                  f"l{i}.ln1_b": a(s + "layernorm_before.bias"),
+                  f"l{i}.qkv_w": np.concatenate([q, k, v], 0).T,
+                  f"l{i}.qkv_b": np.concatenate([qb, kb, vb]),
+                  f"l{i}.out_w": a(s + "attention.o_proj.weight").T,
+                  f"l{i}.out_b": a(s + "attention.o_proj.bias"),
+                  f"l{i}.ln2_g": a(s + "layernorm_after.weight"),
+                  f"l{i}.ln2_b": a(s + "layernorm_after.bias"),
+                  f"l{i}.fc1_w": a(s + "mlp.fc1.weight").T, f"l{i}.fc1_b": a(s + "mlp.fc1.bias"),
+                  f"l{i}.fc2_w": a(s + "mlp.fc2.weight").T, f"l{i}.fc2_b": a(s + "mlp.fc2.bias")})
+    return {k: np.ascontiguousarray(v) for k, v in p.items()}
 
 
 _NAMED = {

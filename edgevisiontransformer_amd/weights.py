@@ -134,6 +134,45 @@ def make_vit_params(cfg: ViTConfig, seed: int = 0) -> Dict[str, np.ndarray]:
     return params
 
 
+def std_vit_param_shapes(cfg: ViTConfig) -> List[tuple]:
+    """(name, shape) list of the STANDARD-semantics ViT (timm / HF DeiT; EVT_VIT_STANDARD in
+    include/evt.h): the reference order plus a qkv bias per layer, and a final LayerNorm + one
+    Linear head instead of the two-layer mlp_head."""
+    d = cfg.dim
+    out = [("patch_w", (cfg.patch_dim, d)), ("patch_b", (d,)), ("cls", (d,)),
+           ("pos", (cfg.tokens, d))]
+    for i in range(cfg.depth):
+        inner = cfg.heads[i] * cfg.head_dim[i]
+        f = cfg.ffn[i]
+        out += [(f"l{i}.ln1_g", (d,)), (f"l{i}.ln1_b", (d,)),
+                (f"l{i}.qkv_w", (d, 3 * inner)), (f"l{i}.qkv_b", (3 * inner,)),
+                (f"l{i}.out_w", (inner, d)), (f"l{i}.out_b", (d,)),
+                (f"l{i}.ln2_g", (d,)), (f"l{i}.ln2_b", (d,)),
+                (f"l{i}.fc1_w", (d, f)), (f"l{i}.fc1_b", (f,)),
+                (f"l{i}.fc2_w", (f, d)), (f"l{i}.fc2_b", (d,))]
+    out += [("norm_g", (d,)), ("norm_b", (d,)), ("head_w", (d, cfg.num_classes)),
+            ("head_b", (cfg.num_classes,))]
+    return out
+
+
+def make_std_vit_params(cfg: ViTConfig, seed: int = 0) -> Dict[str, np.ndarray]:
+    """Seeded fp32 parameters of a standard ViT (same init families as make_vit_params)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    params: Dict[str, np.ndarray] = {}
+    for name, shape in std_vit_param_shapes(cfg):
+        leaf = name.split(".")[-1]
+        if leaf.endswith("_w"):
+            v = _glorot(rng, shape[0], shape[1])
+        elif leaf.endswith("_g"):
+            v = 1.0 + rng.normal(0.0, 0.02, size=shape)
+        elif leaf in ("cls", "pos"):
+            v = rng.normal(0.0, 0.05, size=shape)
+        else:
+            v = rng.normal(0.0, 0.02, size=shape)
+        params[name] = np.ascontiguousarray(v, dtype=np.float32)
+    return params
+
+
 @dataclass(frozen=True)
 class T2TConfig:
     """Static shape of a `T2T_ViT` (reference `modeling/models/t2t_vit.py:91-114`).

@@ -56,7 +56,20 @@ typedef struct evt_vit_desc {
   const int32_t* ffn;      /* [depth] FFN width per layer (ffn.py:5) */
   int32_t dtype;        /* EVT_DTYPE_* */
   int32_t max_batch;    /* workspace is sized for this many images */
+  int32_t semantics;    /* EVT_VIT_REFERENCE (0, the reference Keras model) or EVT_VIT_STANDARD */
+  float layer_norm_eps; /* LayerNorm epsilon; 0 = 1e-5 (Keras / reference norm.py:6) */
 } evt_vit_desc;
+
+/* evt_vit_desc.semantics.
+ * EVT_VIT_REFERENCE: exactly modeling/models/vit.py: block returns f(LN(x)) + LN(x) (norm.py:11-12
+ *   + residual.py:9), QKV without bias, tanh GELU, no final LayerNorm, mlp_head = Dense(M, gelu)
+ *   -> Dense(C) on token 0.
+ * EVT_VIT_STANDARD: the published DeiT / ViT (timm VisionTransformer, HF DeiTModel; what the
+ *   reference loads for accuracy, utils.py:52-62): x + f(LN(x)), QKV with bias, exact (erf) GELU,
+ *   final LayerNorm, one Linear head on token 0 (mlp_dim unused). Weight order in
+ *   evt_vit_num_weights. */
+#define EVT_VIT_REFERENCE 0
+#define EVT_VIT_STANDARD 1
 
 typedef struct evt_model evt_model;
 
@@ -68,9 +81,11 @@ const char* evt_last_error(void);
 
 /* Number of fp32 weight tensors evt_vit_create expects for `desc`, in order:
  *   patch_w [p*p*c, D], patch_b [D], cls [D], pos [P+1, D],
- *   per layer i: ln1_g [D], ln1_b [D], qkv_w [D, 3*h*hk], out_w [h*hk, D], out_b [D],
+ *   per layer i: ln1_g [D], ln1_b [D], qkv_w [D, 3*h*hk], (STANDARD: qkv_b [3*h*hk],)
+ *                out_w [h*hk, D], out_b [D],
  *                ln2_g [D], ln2_b [D], fc1_w [D, F], fc1_b [F], fc2_w [F, D], fc2_b [D],
- *   head1_w [D, M], head1_b [M], head2_w [M, C], head2_b [C].
+ *   REFERENCE: head1_w [D, M], head1_b [M], head2_w [M, C], head2_b [C];
+ *   STANDARD:  norm_g [D], norm_b [D], head_w [D, C], head_b [C].
  * Kernels are Keras Dense layout [in, out] (y = x @ W + b). Replaces the weight creation of
  * ViT.__init__ (vit.py:18-39) + TransformerEncoderBlock(_Pruned).__init__ (transformer_encoder.py:9-36). */
 int evt_vit_num_weights(const evt_vit_desc* desc);

@@ -113,3 +113,30 @@ def vit_forward(params: Dict[str, np.ndarray], cfg, img: np.ndarray,
     t = x[:, 0]                                                        # :54
     h = gelu(t @ P["head1_w"] + P["head1_b"])                          # :55 mlp_head[0]
     return h @ P["head2_w"] + P["head2_b"]                             # :55 mlp_head[1]
+
+
+def std_vit_forward(params: Dict[str, np.ndarray], cfg, img: np.ndarray, eps: float = 1e-6,
+                    dtype=np.float64) -> np.ndarray:
+    """The STANDARD DeiT / ViT forward (EVT_VIT_STANDARD; timm VisionTransformer, HF
+    ViTForImageClassification): x + attn(LN1 x), x + mlp(LN2 x) with QKV bias and exact GELU,
+    final LayerNorm, Linear head on token 0. Patch vectors in this build's (p1 p2 c) order.
+    Pinned by tests/golden/std_*.npz (HF transformers, fp64). TEST INFRASTRUCTURE ONLY."""
+    from scipy.special import erf
+    P = {k: np.asarray(v, dtype=dtype) for k, v in params.items()}
+    x = patchify_nchw(np.asarray(img, dtype=dtype), cfg.patch_size) @ P["patch_w"] + P["patch_b"]
+    b = x.shape[0]
+    x = np.concatenate([np.broadcast_to(P["cls"], (b, 1, cfg.dim)), x], axis=1) + P["pos"]
+    for i in range(cfg.depth):
+        h, hk = cfg.heads[i], cfg.head_dim[i]
+        y = layer_norm(x, P[f"l{i}.ln1_g"], P[f"l{i}.ln1_b"], eps)
+        n = y.shape[1]
+        qkv = (y @ P[f"l{i}.qkv_w"] + P[f"l{i}.qkv_b"]).reshape(b, n, 3, h, hk).transpose(2, 0, 3, 1, 4)
+        att = softmax(np.einsum("bhid,bhjd->bhij", qkv[0], qkv[1]) * hk ** -0.5)
+        o = np.einsum("bhij,bhjd->bhid", att, qkv[2]).transpose(0, 2, 1, 3).reshape(b, n, h * hk)
+        x = x + o @ P[f"l{i}.out_w"] + P[f"l{i}.out_b"]
+        y = layer_norm(x, P[f"l{i}.ln2_g"], P[f"l{i}.ln2_b"], eps)
+        z = y @ P[f"l{i}.fc1_w"] + P[f"l{i}.fc1_b"]
+        z = 0.5 * z * (1.0 + erf(z / math.sqrt(2.0)))
+        x = x + z @ P[f"l{i}.fc2_w"] + P[f"l{i}.fc2_b"]
+    x = layer_norm(x[:, 0], P["norm_g"], P["norm_b"], eps)
+    return x @ P["head_w"] + P["head_b"]

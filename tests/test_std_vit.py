@@ -1,0 +1,71 @@
+"""STANDARD DeiT / ViT semantics (EVT_VIT_STANDARD): oracle vs the HF-produced fp64 goldens (CPU),
+checkpoint mapping round trips (CPU), and the HIP path vs the goldens (GPU; f32 max-abs <= 1e-3,
+bf16 max-abs <= 5e-2 and per-row cosine >= 0.999)."""
+import os
+
+import numpy as np
+import pytest
+
+from edgevisiontransformer_amd.modeling.models import vit as vitmod
+from edgevisiontransformer_amd.weights import digest
+from oracle.vit_ref import std_vit_forward
+from tests.golden.make_golden_std import CASES, EPS, case, hf_state_dict
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_std_oracle_matches_golden(name):
+    cfg, params, img = case(name)
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    assert digest(params) == str(z["param_digest"]) and digest([img]) == str(z["image_digest"])
+    assert np.abs(std_vit_forward(params, cfg, img, eps=EPS) - z["logits"]).max() < 1e-9
+
+
+def test_hf_and_timm_state_dict_mapping():
+    cfg, params, _ = case("std_small4_b3")
+    sd = {k: v.numpy() for k, v in hf_state_dict(params, cfg).items()}
+    back = vitmod.params_from_hf_state_dict(sd, cfg.depth)
+    assert set(back) == set(params)
+    for k in params:
+        assert np.allclose(back[k], params[k], rtol=0, atol=0), k
+    d = cfg.dim
+    timm = {"patch_embed.proj.weight": sd["vit.embeddings.patch_embeddings.projection.weight"],
+            "patch_embed.proj.bias": params["patch_b"], "cls_token": params["cls"].reshape(1, 1, d),
+            "pos_embed": params["pos"][None], "norm.weight": params["norm_g"],
+            "norm.bias": params["norm_b"], "head.weight": params["head_w"].T,
+            "head.bias": params["head_b"]}
+    for i in range(cfg.depth):
+        s = f"blocks.{i}."
+        timm.update({s + "norm1.weight": params[f"l{i}.ln1_g"], s + "norm1.bias": params[f"l{i}.ln1_b"],
+                     s + "attn.qkv.weight": params[f"l{i}.qkv_w"].T, s + "attn.qkv.bias": params[f"l{i}.qkv_b"],
+                     s + "attn.proj.weight": params[f"l{i}.out_w"].T, s + "attn.proj.bias": params[f"l{i}.out_b"],
+                     s + "norm2.weight": params[f"l{i}.ln2_g"], s + "norm2.bias": params[f"l{i}.ln2_b"],
+                     s + "mlp.fc1.weight": params[f"l{i}.fc1_w"].T, s + "mlp.fc1.bias": params[f"l{i}.fc1_b"],
+                     s + "mlp.fc2.weight": params[f"l{i}.fc2_w"].T, s + "mlp.fc2.bias": params[f"l{i}.fc2_b"]})
+    back = vitmod.params_from_timm_state_dict(timm, cfg.depth)
+    for k in params:
+        assert np.array_equal(back[k], params[k]), k
+
+
+def _cos_rows(a, b):
+    return (a * b).sum(1) / (np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(CASES))
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_std_vit_gpu(gpu, name, dtype):
+    import torch
+    cfg, params, img = case(name)
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    m = vitmod.StandardViT(dim=cfg.dim, depth=cfg.depth, heads=cfg.heads[0],
+                           mlp_ratio=cfg.ffn[0] / cfg.dim, num_classes=cfg.num_classes,
+                           layer_norm_eps=EPS, dtype=dtype, weights=params, device=gpu)
+    out = m(torch.from_numpy(img).to(gpu)).cpu().numpy().astype(np.float64)
+    err = np.abs(out - z["logits"]).max()
+    if dtype == "f32":
+        assert err <= 1e-3, err
+    else:
+        assert err <= 5e-2, err
+        assert _cos_rows(out, z["logits"]).min() >= 0.999
