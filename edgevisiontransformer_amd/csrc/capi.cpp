@@ -1005,6 +1005,14 @@ int evt_swin_forward(evt_model* m, const float* img, int B, float* logits, void*
         c.resid = m->x; c.ldr = Cst; c.stats_out = m->sm; c.ln_width = C;
         EVT_RC(dense(m, bl.proj, c, s));
       }
+      if (dt == DT_BF16 && C == 96 && st.mlp == 384 && gemm_variant() == 0) {
+        // stage-1 MLP (C = 96) fused: hidden kept on chip (swin.hip, swin_mlp96_kernel)
+        SwinMlpParams mp{m->xm, m->x, m->sm, m->sx, bl.fc1.w, bl.fc1.colsum, bl.fc1.b,
+                         bl.fc2.w, bl.fc2.b, bl.fc1.kpad, bl.fc2.kpad, rows, stats_slots(C),
+                         m->eps};
+        EVT_HIP(swin_mlp96_launch(mp, s), "fused MLP");
+        continue;
+      }
       {  // LN2-folded FC1 + erf GELU
         DenseCall c;
         c.flags = EPI_LNIN | EPI_BIAS | EPI_GELU_ERF;

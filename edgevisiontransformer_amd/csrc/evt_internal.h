@@ -139,4 +139,22 @@ hipError_t ln_pool_launch(int dtype, const void* x, int64_t ldx, int B, int T, i
                           const float* stats, int nslots, const float* gamma, const float* beta,
                           void* out, int64_t ldo, hipStream_t s);
 
+// Fused Swin MLP of a C = 96 stage (bf16): x = xm + FC2(GELU(FC1(LN2(xm)))) + row statistics.
+struct SwinMlpParams {
+  const void* xm;          // [M][96] block input (bf16)
+  void* x;                 // [M][96] block output (bf16)
+  const float* stats_in;   // [M][nslots][2] statistics of the xm rows (LN2)
+  float* stats_out;        // [M][nslots][2] statistics of the x rows (slot 0 total, rest 0)
+  const void* w1;          // FC1 packed [>= 384][ldw1] bf16, LN2 gamma folded
+  const float* colsum;     // [384] FC1 LN-fold column sums
+  const float* cvec;       // [384] FC1 beta.W + bias
+  const void* w2;          // FC2 packed [>= 96][ldw2] bf16 (K = hidden)
+  const float* b2;         // [96]
+  int64_t ldw1, ldw2;
+  int M, nslots;
+  float eps;
+};
+hipError_t swin_mlp96_launch(const SwinMlpParams& p, hipStream_t s);
+int gemm_variant();  // the process-wide evt_set_gemm_variant value (0 = automatic)
+
 }  // namespace evt

@@ -161,7 +161,8 @@ __device__ __forceinline__ void epi_rows_t(const GemmParams& p, EVT_LDS char* st
     } else if (FL & EPI_BIAS) {
       v += bias4;
     }
-    if (FL & (EPI_GELU | EPI_GELU_ERF)) v = gelu4(v, (FL & EPI_GELU_ERF) != 0);
+    if (FL & (EPI_GELU | EPI_GELU_ERF))
+      v = gelu4(v, (FL & EPI_GELU) ? 0 : std::is_same<T, bf16>::value ? 2 : 1);
     if (FL & EPI_POS) {
       const int img = m / p.P, t = m - img * p.P;
       orow = (int64_t)img * (p.P + 1) + 1 + t;
@@ -289,7 +290,7 @@ __device__ __forceinline__ void epi_rows8_t(const GemmParams& p, EVT_LDS char* s
     }
     if (FL & (EPI_GELU | EPI_GELU_ERF)) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) v[h] = gelu4(v[h], (FL & EPI_GELU_ERF) != 0);
+      for (int h = 0; h < 2; ++h) v[h] = gelu4(v[h], (FL & EPI_GELU) ? 0 : 2);  // bf16 only
     }
     if (FL & EPI_POS) {
       const int img = m / p.P, t = m - img * p.P;
@@ -948,7 +949,7 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
       // column group past N (padding of the packed width): wave-uniform skip of the VALU work
       if (PADN && !interior && n0 + wn * 64 + nt * 16 >= p.N) continue;
 #pragma unroll
-      for (int mt = 0; mt < 8; ++mt) acc[nt][mt] = gelu4(acc[nt][mt], (FL & EPI_GELU_ERF) != 0);
+      for (int mt = 0; mt < 8; ++mt) acc[nt][mt] = gelu4(acc[nt][mt], (FL & EPI_GELU) ? 0 : 2);
     }
   }
   // 2. store layout: pair (2k, 2k+1) -> lane row wm*128 + (2k + (fg & 1))*16 + frow, columns
@@ -1471,6 +1472,7 @@ __global__ void fold_kernel(const T* __restrict__ Wp, int Kpad, const float* __r
 }  // namespace
 
 void gemm_set_variant(int v) { g_gemm_variant = v; }
+int gemm_variant() { return g_gemm_variant; }
 
 size_t gemm_sk_bytes() { return 4096 + (size_t)SK_MAX_G * SK_SLOT_FLOATS * sizeof(float); }
 

@@ -434,6 +434,155 @@ __global__ __launch_bounds__(256) void ln_pool_kernel(const T* __restrict__ x, i
   }
 }
 
+// ---- fused MLP of the C = 96 stage (Swin-T / Swin-S stage 1) -------------------------------
+// x = xm + fc2(GELU(LN2(xm) W1 + b1)) + b2 (+ row statistics of x) in one pass: the 384-wide
+// hidden never leaves the CU. The separate GEMMs move 1.7 GB per stage-1 block (FC1 writes the
+// 617 MB hidden, FC2 reads it back) and serialise the erf-GELU VALU work behind the tiles' MFMA;
+// here it is xm in + x out (0.3 GB) and each SIMD runs two waves whose MFMA and VALU phases
+// interleave.
+//   LDS (whole block, loaded once): W1 = the LN2-folded FC1 weights, 384 hidden rows x 96 k
+//   (208-B rows: the 16 lanes of one k chunk hit distinct 4-bank groups), and W2 = FC2, 96 output
+//   rows x 384 hidden (784-B rows) with the hidden axis permuted per 32-chunk so that the FC1
+//   accumulators ARE the FC2 B operand: chunk position 8g + s holds hidden 4g + s (s < 4) or
+//   16 + 4g + (s - 4) - the two 16-row FC1 tiles of the chunk, as lane group g holds them.
+//   Wave = 32 tokens (2 tiles of 16), their rows normalised once in registers ((x - mu) r; gamma
+//   folded into W1). Per 32-hidden chunk: H^T = W1 . LN(xm)^T seeded with beta.W1 + b1 (12 MFMAs),
+//   GELU on the 16 accumulators per lane, bf16 pack, Out^T += W2 . H^T (12 MFMAs, seeded with b2).
+//   Products are transposed (C^T = A . B) so one token is one lane column throughout. The
+//   per-lane VALU work (GELU) is the bound: erf GELU in its fast bf16-path form.
+constexpr int MLP96_C = 96, MLP96_F = 384;
+constexpr int MLP96_W1_ROW = 208, MLP96_W2_ROW = 784;
+constexpr int MLP96_LDS = MLP96_F * MLP96_W1_ROW + MLP96_C * MLP96_W2_ROW;  // 155136 B
+
+__global__ __launch_bounds__(512, 1) void swin_mlp96_kernel(SwinMlpParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  EVT_LDS char* W1s = (EVT_LDS char*)smem;
+  EVT_LDS char* W2s = W1s + MLP96_F * MLP96_W1_ROW;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const bf16* w1 = (const bf16*)p.w1;
+  const bf16* w2 = (const bf16*)p.w2;
+  // ---- stage the weights (once per block) ----
+  for (int e = tid; e < MLP96_F * 12; e += 512) {  // W1: row n, 16-B chunk j of 12
+    const int n = e / 12, j = e - n * 12;
+    *(EVT_LDS u32x4*)(W1s + n * MLP96_W1_ROW + j * 16) = *(const u32x4*)(w1 + (int64_t)n * p.ldw1 + j * 8);
+  }
+  for (int e = tid; e < MLP96_C * 48; e += 512) {  // W2: row c, chunk (hc, gg) of 12 x 4
+    const int c = e / 48, r = e - c * 48, hc = r >> 2, gg = r & 3;
+    const bf16* src = w2 + (int64_t)c * p.ldw2 + hc * 32 + 4 * gg;
+    const uint2 lo = *(const uint2*)src;         // hidden 32 hc + 4 gg .. + 3
+    const uint2 hi = *(const uint2*)(src + 16);  // hidden 32 hc + 16 + 4 gg .. + 3
+    *(EVT_LDS u32x4*)(W2s + c * MLP96_W2_ROW + hc * 64 + gg * 16) = u32x4{lo.x, lo.y, hi.x, hi.y};
+  }
+  __syncthreads();
+  const float inv_d = 1.0f / (float)MLP96_C;
+  const int ntiles = (p.M + 31) / 32;
+  for (int t = blockIdx.x * 8 + wave; t < ntiles; t += gridDim.x * 8) {
+    const int tok0 = t * 32;
+    // B operand of FC1: LN2(xm) of token (16 tt + c16), k 32 ks + 8 g .. + 7, normalised in
+    // registers ((x - mu) r; gamma is folded into W1, beta.W1 + b1 = cvec seeds the accumulator)
+    u32x4 a[2][3];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int m = min(tok0 + 16 * tt + c16, p.M - 1);
+      const bf16* ar = (const bf16*)p.xm + (int64_t)m * MLP96_C;
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) a[tt][ks] = *(const u32x4*)(ar + 32 * ks + 8 * g);
+      const float* st = p.stats_in + (int64_t)m * 2 * p.nslots;
+      float s1 = 0.f, s2 = 0.f;
+      for (int j = 0; j < p.nslots; ++j) {
+        s1 += st[2 * j];
+        s2 += st[2 * j + 1];
+      }
+      const float mu = s1 * inv_d;
+      const float rs = rsqrtf(fmaxf(s2 * inv_d - mu * mu, 0.f) + p.eps);
+      const f32x2 r2 = {rs, rs}, o2 = {-mu * rs, -mu * rs};
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        const bf16x8 xv = __builtin_bit_cast(bf16x8, a[tt][ks]);
+        u32x4 nv;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x2 f = f32x2{(float)xv[2 * q], (float)xv[2 * q + 1]} * r2 + o2;
+          nv[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(f, bf16x2));
+        }
+        a[tt][ks] = nv;
+      }
+    }
+    f32x4 out[6][2];
+#pragma unroll
+    for (int ct = 0; ct < 6; ++ct) out[ct][0] = out[ct][1] = load4(p.b2 + ct * 16 + 4 * g);
+#pragma unroll 2
+    for (int hc = 0; hc < 12; ++hc) {
+      f32x4 h[2][2];
+#pragma unroll
+      for (int ht = 0; ht < 2; ++ht) {
+        const EVT_LDS char* wr = W1s + (hc * 32 + ht * 16 + c16) * MLP96_W1_ROW + 16 * g;
+        h[ht][0] = h[ht][1] = load4(p.cvec + hc * 32 + ht * 16 + 4 * g);
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) {
+          const u32x4 wv = *(const EVT_LDS u32x4*)(wr + 64 * ks);
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt)
+            h[ht][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8, wv), __builtin_bit_cast(bf16x8, a[tt][ks]), h[ht][tt], 0, 0, 0);
+        }
+      }
+      // h[ht][tt][jj]: hidden 32 hc + 16 ht + 4 g + jj, token 16 tt + c16 (bias included) -> GELU,
+      // packed straight into the FC2 B operand (k slots 8 g .. 8 g + 7 = [ht 0 jj 0..3 | ht 1])
+      u32x4 pf[2];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht) {
+          const f32x2 lo = gelu_erf_fast2(f32x2{h[ht][tt][0], h[ht][tt][1]});
+          const f32x2 hi = gelu_erf_fast2(f32x2{h[ht][tt][2], h[ht][tt][3]});
+          pf[tt][2 * ht] = __builtin_bit_cast(unsigned, __builtin_convertvector(lo, bf16x2));
+          pf[tt][2 * ht + 1] = __builtin_bit_cast(unsigned, __builtin_convertvector(hi, bf16x2));
+        }
+#pragma unroll
+      for (int ct = 0; ct < 6; ++ct) {
+        const u32x4 wv = *(const EVT_LDS u32x4*)(W2s + (ct * 16 + c16) * MLP96_W2_ROW + hc * 64 + 16 * g);
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+          out[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, wv), __builtin_bit_cast(bf16x8, pf[tt]), out[ct][tt], 0, 0, 0);
+      }
+    }
+    // out[ct][tt][jj]: feature 16 ct + 4 g + jj, token 16 tt + c16: + b2 + xm, store x, stats
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int m = tok0 + 16 * tt + c16;
+      const bool ok = m < p.M;
+      const int mc = min(m, p.M - 1);
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int ct = 0; ct < 6; ++ct) {
+        const int c = ct * 16 + 4 * g;
+        const f32x4 r = load4((const bf16*)p.xm + (int64_t)mc * MLP96_C + c);
+        const f32x4 v = out[ct][tt] + r;  // (b2 seeded the accumulator)
+        const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        if (ok) *(bf16x4*)((bf16*)p.x + (int64_t)m * MLP96_C + c) = o;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const float f = (float)o[jj];
+          s1 += f;
+          s2 += f * f;
+        }
+      }
+      s1 += __shfl_xor(s1, 16, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (ok && g < p.nslots) {
+        float* so = p.stats_out + (int64_t)m * 2 * p.nslots + 2 * g;
+        so[0] = g == 0 ? s1 : 0.f;
+        so[1] = g == 0 ? s2 : 0.f;
+      }
+    }
+  }
+}
+
 template <typename T, int LPR, int NC>
 hipError_t ln_rows_lc(const void* x, int64_t ld, void* y, const float* g, const float* bb,
                       int rows, int D, float eps, float* stats, int nslots, hipStream_t s) {
@@ -519,6 +668,25 @@ hipError_t window_attn_launch(int dtype, const SwinAttnParams& p, hipStream_t s)
     hipLaunchKernelGGL(window_attn_bf16_kernel, grid, dim3(256), 0, s, p);
   else
     hipLaunchKernelGGL(window_attn_f32_kernel, grid, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t swin_mlp96_launch(const SwinMlpParams& p, hipStream_t s) {
+  if (p.M <= 0) return hipSuccess;
+  if (p.nslots < 1 || p.nslots > 4 || p.ldw1 < MLP96_C || p.ldw2 < MLP96_F || p.ldw1 % 8 ||
+      p.ldw2 % 8)
+    return hipErrorInvalidValue;
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipFuncSetAttribute((const void*)swin_mlp96_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, MLP96_LDS);
+  }
+  const int waves = (p.M + 31) / 32;
+  const int grid = std::max(1, std::min(ncu, (waves + 7) / 8));
+  hipLaunchKernelGGL(swin_mlp96_kernel, dim3(grid), dim3(512), MLP96_LDS, s, p);
   return hipGetLastError();
 }
 

@@ -134,3 +134,22 @@ def test_patch_merge_kernel(gpu, dtype):
     assert np.allclose(st[:, 0, 0], ref.astype(np.float64).sum(1), rtol=1e-5, atol=1e-3)
     assert np.allclose(st[:, 0, 1], (ref.astype(np.float64) ** 2).sum(1), rtol=1e-5, atol=1e-3)
     assert (st[:, 1:] == 0).all()
+
+
+def test_fused_stage1_mlp_matches_gemm_path(gpu):
+    """The fused C = 96 MLP kernel (default) against the two-GEMM path (forced by any explicit GEMM
+    variant) on the same model and images: same math, different bf16 rounding points."""
+    cfg = swin_config("tiny", image_size=56, depths=(2, 2), num_heads=(3, 6), num_classes=37)
+    params = make_swin_params(cfg, seed=15)
+    m = _model(cfg, "bf16", params, gpu, max_batch=6)
+    img = torch.from_numpy(make_images(6, seed=16, image_size=56)).to(gpu)
+    lib = _lib.load_library()
+    fused = m(img).cpu().numpy().astype(np.float64)
+    _lib.check(lib.evt_set_gemm_variant(9))
+    try:
+        gemm = m(img).cpu().numpy().astype(np.float64)
+    finally:
+        _lib.check(lib.evt_set_gemm_variant(0))
+    ref = swin_ref.swin_forward(params, cfg, make_images(6, seed=16, image_size=56))
+    assert np.abs(fused - gemm).max() <= 3e-2
+    assert np.abs(fused - ref).max() <= 5e-2 and _cos_rows(fused, ref).min() >= 0.999
