@@ -121,7 +121,7 @@ hipError_t cls_rows_launch(int dtype, void* x, int B, int ntok, int D, const flo
 struct SwinAttnParams {
   const void* qkv; int64_t ldq;   // raster-order token rows [B*R*R], columns (qkv h d), head 32
   void* out;       int64_t ldo;   // raster-order rows, columns (h d); [C, ldo) written as 0
-  const float* bias;              // [H][49][64] relative position bias * log2(e), -inf past 49
+  const float* bias;              // [types][H][49][64] bias + shift mask, * log2(e); -inf past 49
   int B, R, nwx, C, H;            // images, resolution, windows per row (R / 7), channels, heads
   int shift;                      // cyclic shift (0: W-MSA, 3: SW-MSA with the region mask)
   float scale_log2;               // 32^-0.5 * log2(e)
@@ -133,7 +133,9 @@ hipError_t ln_rows_launch(int dtype, const void* x, int64_t ld, void* y, const f
                           hipStream_t s);
 hipError_t merge_launch(int dtype, const void* x, int64_t ldx, int B, int R, int C, void* out,
                         float* stats, int nslots, hipStream_t s);
-hipError_t rpb_dense_launch(const float* table, int H, int w, float* dense, hipStream_t s);
+// dense bias+mask tables [types][H][49][64] (types = 4 when shift > 0, else 1)
+hipError_t rpb_dense_launch(const float* table, int H, int w, int shift, float* dense,
+                            hipStream_t s);
 hipError_t window_attn_launch(int dtype, const SwinAttnParams& p, hipStream_t s);
 hipError_t ln_pool_launch(int dtype, const void* x, int64_t ldx, int B, int T, int D,
                           const float* stats, int nslots, const float* gamma, const float* beta,

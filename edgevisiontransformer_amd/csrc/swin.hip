@@ -16,7 +16,8 @@
 //                        into the reduction GEMM)
 //   window_attn_bf16     one wave per (window, head): S^T = K Q^T and O^T = V^T P^T on
 //                        v_mfma_f32_16x16x32_bf16 (head size 32 = one MFMA k-step), + relative
-//                        position bias, + SW-MSA mask from the region ids, exact softmax
+//                        position bias + SW-MSA mask (one precomputed table per window type),
+//                        exact softmax
 //   window_attn_f32      the exact fp32 parity path (VALU dot products, K / V in LDS)
 //   ln_pool_kernel       final LayerNorm + mean over tokens (AdaptiveAvgPool1d) -> [B][Cst]
 #include <algorithm>
@@ -118,10 +119,21 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(const T* __restrict__ x, i
     const int c0 = (i * LPR + sub) * V;
     if (c0 >= ld) continue;
     T o[V];
+    float gv[V], bv[V];  // 16-B loads of gamma / beta (D is a multiple of V here)
+#pragma unroll
+    for (int j = 0; j < V; j += 4) {
+      const f32x4 gq = c0 + j < D ? load4(gamma + c0 + j) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 bq = c0 + j < D ? load4(beta + c0 + j) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        gv[j + u] = gq[u];
+        bv[j + u] = bq[u];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       const int c = c0 + j;
-      o[j] = from_f32<T>(c < D ? (v[i][j] - mean) * rstd * gamma[c] + beta[c] : 0.f);
+      o[j] = from_f32<T>(c < D ? (v[i][j] - mean) * rstd * gv[j] + bv[j] : 0.f);
       const float f = to_f32(o[j]);
       s1 += f;
       s2 += f * f;
@@ -178,24 +190,34 @@ __global__ __launch_bounds__(256) void merge_kernel(const T* __restrict__ x, int
   }
 }
 
-// ---- relative position bias, expanded once per block at model creation ----------------------
-// dense[h][q][k] = table[(qy-ky+w-1)*(2w-1) + (qx-kx+w-1)][h] * log2(e) for k < w*w, -inf after.
-__global__ void rpb_dense_kernel(const float* __restrict__ table, int H, int w,
+// ---- relative position bias + shift mask, expanded once per block at model creation ----------
+// dense[type][h][q][k] = table[(qy-ky+w-1)*(2w-1) + (qx-kx+w-1)][h] * log2(e), -100 * log2(e) more
+// where q and k lie in different SW-MSA regions, -inf for k >= w*w. With a shift the windows of
+// the last window row / column see the 3x3 region split (region of a window-local row i: 1 if
+// i < w - shift else 2; 0 elsewhere): type = 2 * (last window row) + (last window column).
+// Without a shift there is one type (no mask).
+__global__ void rpb_dense_kernel(const float* __restrict__ table, int H, int w, int shift,
                                  float* __restrict__ dense) {
   const int n = w * w;
+  const int ntypes = shift ? 4 : 1;
   const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= H * n * 64) return;
-  const int h = e / (n * 64), r = e - h * n * 64, q = r / 64, k = r - q * 64;
+  if (e >= ntypes * H * n * 64) return;
+  const int type = e / (H * n * 64), r0 = e - type * H * n * 64;
+  const int h = r0 / (n * 64), r = r0 - h * n * 64, q = r / 64, k = r - q * 64;
   float v = -INFINITY;
   if (k < n) {
     const int qy = q / w, qx = q - qy * w, ky = k / w, kx = k - ky * w;
     v = table[((qy - ky + w - 1) * (2 * w - 1) + (qx - kx + w - 1)) * H + h] * kLog2e;
+    const bool lr = type & 2, lc = type & 1;  // last window row / column
+    const int rq = (lr ? (qy < w - shift ? 1 : 2) : 0) * 3 + (lc ? (qx < w - shift ? 1 : 2) : 0);
+    const int rk = (lr ? (ky < w - shift ? 1 : 2) : 0) * 3 + (lc ? (kx < w - shift ? 1 : 2) : 0);
+    if (rq != rk) v += -100.0f * kLog2e;
   }
   dense[e] = v;
 }
 
 // Row of window-local token t (t < 49) of window `win` of image b, with the cyclic shift; and
-// its SW-MSA region id (3x3 regions of the shifted frame).
+// the bias / mask table type of the window.
 struct WinGeom {
   int R, nwx, s;
   __device__ __forceinline__ int64_t row(int b, int win, int t) const {
@@ -206,13 +228,11 @@ struct WinGeom {
     if (x >= R) x -= R;
     return (int64_t)b * R * R + (int64_t)y * R + x;
   }
-  __device__ __forceinline__ int region(int win, int t) const {
+  // bias/mask table type of a window (rpb_dense_kernel): last window row / column when shifted
+  __device__ __forceinline__ int type(int win) const {
+    if (!s) return 0;
     const int wy = win / nwx, wx = win - wy * nwx;
-    const int i = t / 7, j = t - i * 7;
-    const int ys = wy * 7 + i, xs = wx * 7 + j;
-    const int rh = ys < R - 7 ? 0 : (ys < R - s ? 1 : 2);
-    const int rw = xs < R - 7 ? 0 : (xs < R - s ? 1 : 2);
-    return rh * 3 + rw;
+    return (wy == nwx - 1 ? 2 : 0) + (wx == nwx - 1 ? 1 : 0);
   }
 };
 
@@ -244,26 +264,17 @@ __global__ __launch_bounds__(256) void window_attn_bf16_kernel(SwinAttnParams p)
   // Q and K fragments: tile i, lane (token 16 i + c16, d 8 g .. 8 g + 7)
   u32x4 qf[4], kf[4];
   int64_t qrow[4];
-  int qreg[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int t = min(16 * i + c16, 48);
     qrow[i] = G.row(b, win, t);
-    qreg[i] = G.region(win, t);
     const bf16* rp = qkv + qrow[i] * p.ldq + h * 32 + 8 * g;
     qf[i] = *(const u32x4*)rp;
     kf[i] = *(const u32x4*)(rp + p.C);
   }
-  // key regions of this lane's 16 keys (key 16 kt + 4 g + j)
-  int kreg[4][4];
-#pragma unroll
-  for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) kreg[kt][j] = G.region(win, min(16 * kt + 4 * g + j, 48));
   wait_vmcnt0();
 
-  const float mval = -100.0f * kLog2e;
-  const float* bias_h = p.bias + (int64_t)h * 49 * 64;
+  const float* bias_h = p.bias + ((int64_t)G.type(win) * p.H + h) * 49 * 64;
   const int tq = (lane >> 2) & 3, tp = lane & 3;
 #pragma unroll
   for (int qt = 0; qt < 4; ++qt) {
@@ -276,20 +287,21 @@ __global__ __launch_bounds__(256) void window_attn_bf16_kernel(SwinAttnParams p)
                                                       __builtin_bit_cast(bf16x8, qf[qt]), acc, 0,
                                                       0, 0);
     }
-    // s[kt][j] = S^T[key 16 kt + 4 g + j][query q]: scores in the log2 domain + bias (+ mask)
+    // s[kt][j] = S^T[key 16 kt + 4 g + j][query q]: scores in the log2 domain + bias (incl. the
+    // shift mask and -inf past key 49) on packed pairs; max over canonical (computed) values
     const float* br = bias_h + (int64_t)min(q, 48) * 64 + 4 * g;
-    float mx = -INFINITY;
+    const f32x2 sc2 = {p.scale_log2, p.scale_log2};
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
       const f32x4 bv = *(const f32x4*)(br + 16 * kt);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float v = s[kt][j] * p.scale_log2 + bv[j];
-        if (p.shift && kreg[kt][j] != qreg[qt]) v += mval;
-        s[kt][j] = v;
-        mx = fmaxf(mx, v);
-      }
+      const f32x2 lo = f32x2{s[kt][0], s[kt][1]} * sc2 + f32x2{bv[0], bv[1]};
+      const f32x2 hi = f32x2{s[kt][2], s[kt][3]} * sc2 + f32x2{bv[2], bv[3]};
+      s[kt] = f32x4{lo[0], lo[1], hi[0], hi[1]};
     }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+      mx = fmaxf(fmaxf(mx, fmaxf(s[kt][0], s[kt][1])), fmaxf(s[kt][2], s[kt][3]));
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     float sum = 0.f;
@@ -363,11 +375,10 @@ __global__ __launch_bounds__(256) void window_attn_f32_kernel(SwinAttnParams p) 
   __builtin_amdgcn_wave_barrier();
   const int t = min(lane, 48);
   const int64_t qrow = G.row(b, win, t);
-  const int qreg = G.region(win, t);
   float q[32];
 #pragma unroll
   for (int d = 0; d < 32; ++d) q[d] = qkv[qrow * p.ldq + h * 32 + d];
-  const float* br = p.bias + ((int64_t)h * 49 + t) * 64;
+  const float* br = p.bias + (((int64_t)G.type(win) * p.H + h) * 49 + t) * 64;
   float sc[49];
   float mx = -INFINITY;
 #pragma unroll
@@ -375,8 +386,7 @@ __global__ __launch_bounds__(256) void window_attn_f32_kernel(SwinAttnParams p) 
     float a = 0.f;
 #pragma unroll
     for (int d = 0; d < 32; ++d) a += q[d] * Ks[k][d];
-    float v = a * p.scale_log2 + br[k];
-    if (p.shift && G.region(win, k) != qreg) v += -100.0f * kLog2e;
+    const float v = a * p.scale_log2 + br[k];
     sc[k] = v;
     mx = fmaxf(mx, v);
   }
@@ -630,7 +640,8 @@ hipError_t ln_rows_launch(int dtype, const void* x, int64_t ld, void* y, const f
                           const float* beta, int rows, int D, float eps, float* stats, int nslots,
                           hipStream_t s) {
   if (rows <= 0) return hipSuccess;
-  if (D <= 0 || D > ld || ld > 1024 || nslots > 64 || ld % (dtype == DT_BF16 ? 8 : 4))
+  if (D <= 0 || D > ld || ld > 1024 || nslots > 64 || ld % (dtype == DT_BF16 ? 8 : 4) ||
+      D % (dtype == DT_BF16 ? 8 : 4))
     return hipErrorInvalidValue;
   return dtype == DT_BF16 ? ln_rows_t<bf16>(x, ld, y, gamma, beta, rows, D, eps, stats, nslots, s)
                           : ln_rows_t<float>(x, ld, y, gamma, beta, rows, D, eps, stats, nslots, s);
@@ -651,9 +662,11 @@ hipError_t merge_launch(int dtype, const void* x, int64_t ldx, int B, int R, int
   return hipGetLastError();
 }
 
-hipError_t rpb_dense_launch(const float* table, int H, int w, float* dense, hipStream_t s) {
-  const int n = H * w * w * 64;
-  hipLaunchKernelGGL(rpb_dense_kernel, dim3((n + 255) / 256), dim3(256), 0, s, table, H, w, dense);
+hipError_t rpb_dense_launch(const float* table, int H, int w, int shift, float* dense,
+                            hipStream_t s) {
+  const int n = (shift ? 4 : 1) * H * w * w * 64;
+  hipLaunchKernelGGL(rpb_dense_kernel, dim3((n + 255) / 256), dim3(256), 0, s, table, H, w, shift,
+                     dense);
   return hipGetLastError();
 }
 
