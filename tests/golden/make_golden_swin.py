@@ -33,6 +33,9 @@ CASES = {
     "swin_tiny_b1": (dict(variant="tiny"), 1, 11, 12),
     "swin_micro_b2": (dict(variant="tiny", image_size=56, depths=(2, 2), num_heads=(3, 6),
                            num_classes=37), 2, 13, 14),
+    # Swin-B widths (embed 128, heads 4 / 8): the C = 128 stage-1 path (no fused MLP), 3 images
+    "swin_base_micro_b3": (dict(variant="base", image_size=56, depths=(2, 2), num_heads=(4, 8),
+                                num_classes=19), 3, 17, 18),
 }
 
 

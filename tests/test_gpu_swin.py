@@ -34,7 +34,7 @@ def _cos_rows(a, b):
     return (a * b).sum(1) / (np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1))
 
 
-@pytest.mark.parametrize("name", ["swin_micro_b2", "swin_tiny_b1"])
+@pytest.mark.parametrize("name", ["swin_micro_b2", "swin_tiny_b1", "swin_base_micro_b3"])
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 def test_swin_golden(gpu, name, dtype):
     z, cfg, params, img = golden_case(name)

@@ -27,7 +27,7 @@ def golden_case(name):
     return z, cfg, params, img
 
 
-@pytest.mark.parametrize("name", ["swin_micro_b2", "swin_tiny_b1"])
+@pytest.mark.parametrize("name", ["swin_micro_b2", "swin_tiny_b1", "swin_base_micro_b3"])
 def test_oracle_matches_golden(name):
     z, cfg, params, img = golden_case(name)
     trace = {}
