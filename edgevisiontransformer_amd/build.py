@@ -22,6 +22,13 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-re
 #                                every code path (interior / edge tiles) -> batch-independent bits
 
 
+# MFMA results straight into VGPRs: with the default AGPR form the compiler parks the small
+# attention / window-attention / performer accumulators in AGPRs and copies every element back
+# (v_accvgpr_read) before the softmax / GELU VALU work (96 copies per window-attention wave).
+PER_FILE_FLAGS = {s: ["-mllvm", "-amdgpu-mfma-vgpr-form=true"]
+                  for s in ("attention.hip", "swin.hip", "t2t.hip")}
+
+
 def _hipcc() -> str:
     for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
         if c and (os.path.isabs(c) and os.path.exists(c) or not os.path.isabs(c)):
@@ -43,7 +50,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         o = os.path.join(OBJ, src + ".o")
         objs.append(o)
         if force or _mtime(o) < max(_mtime(s), hdr_t):
-            cmd = [_hipcc(), *FLAGS, "-c", s, "-o", o]
+            cmd = [_hipcc(), *FLAGS, *PER_FILE_FLAGS.get(src, []), "-c", s, "-o", o]
             if src.endswith(".cpp"):
                 cmd = [_hipcc(), "-O3", "-std=c++17", "-fPIC", "-c", s, "-o", o]
             jobs.append(cmd)

@@ -219,21 +219,25 @@ __global__ void rpb_dense_kernel(const float* __restrict__ table, int H, int w, 
 // Row of window-local token t (t < 49) of window `win` of image b, with the cyclic shift; and
 // the bias / mask table type of the window.
 struct WinGeom {
-  int R, nwx, s;
-  __device__ __forceinline__ int64_t row(int b, int win, int t) const {
+  int R, s;
+  int y0, x0;       // shifted-frame origin of the window (wy * 7 + s, wx * 7 + s)
+  int64_t base;     // first token row of the image
+  int wtype;        // bias / mask table type (rpb_dense_kernel): last window row / column
+  __device__ __forceinline__ WinGeom(int R_, int nwx, int s_, int b, int win) : R(R_), s(s_) {
     const int wy = win / nwx, wx = win - wy * nwx;
+    y0 = wy * 7 + s;
+    x0 = wx * 7 + s;
+    base = (int64_t)b * R * R;
+    wtype = s ? (wy == nwx - 1 ? 2 : 0) + (wx == nwx - 1 ? 1 : 0) : 0;
+  }
+  __device__ __forceinline__ int64_t row(int t) const {
     const int i = t / 7, j = t - i * 7;
-    int y = wy * 7 + i + s, x = wx * 7 + j + s;
+    int y = y0 + i, x = x0 + j;
     if (y >= R) y -= R;
     if (x >= R) x -= R;
-    return (int64_t)b * R * R + (int64_t)y * R + x;
+    return base + (y * R + x);
   }
-  // bias/mask table type of a window (rpb_dense_kernel): last window row / column when shifted
-  __device__ __forceinline__ int type(int win) const {
-    if (!s) return 0;
-    const int wy = win / nwx, wx = win - wy * nwx;
-    return (wy == nwx - 1 ? 2 : 0) + (wx == nwx - 1 ? 1 : 0);
-  }
+  __device__ __forceinline__ int type() const { return wtype; }
 };
 
 // bf16 window attention. 4 waves per block, wave = one (image, window, head); head size 32,
@@ -249,7 +253,7 @@ __global__ __launch_bounds__(256) void window_attn_bf16_kernel(SwinAttnParams p)
   const int h = (int)(pair % p.H);
   const int64_t bw = pair / p.H;
   const int win = (int)(bw % nw), b = (int)(bw / nw);
-  const WinGeom G{p.R, p.nwx, p.shift};
+  const WinGeom G(p.R, p.nwx, p.shift, b, win);
   const bf16* qkv = (const bf16*)p.qkv;
   const int g = lane >> 4, c16 = lane & 15;
   EVT_LDS char* Vs = (EVT_LDS char*)smem + wave * 4096;
@@ -258,7 +262,7 @@ __global__ __launch_bounds__(256) void window_attn_bf16_kernel(SwinAttnParams p)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = 16 * i + (lane >> 2), ch = (lane & 3) ^ ((r >> 2) & 3);
-    const int64_t gr = G.row(b, win, min(r, 48));
+    const int64_t gr = G.row(min(r, 48));
     glds16(qkv + gr * p.ldq + 2 * p.C + h * 32 + ch * 8, Vs + i * 1024);
   }
   // Q and K fragments: tile i, lane (token 16 i + c16, d 8 g .. 8 g + 7)
@@ -267,14 +271,21 @@ __global__ __launch_bounds__(256) void window_attn_bf16_kernel(SwinAttnParams p)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int t = min(16 * i + c16, 48);
-    qrow[i] = G.row(b, win, t);
+    qrow[i] = G.row(t);
     const bf16* rp = qkv + qrow[i] * p.ldq + h * 32 + 8 * g;
     qf[i] = *(const u32x4*)rp;
     kf[i] = *(const u32x4*)(rp + p.C);
   }
+  // bias + mask rows of all four query tiles, in flight with the Q / K / V loads
+  const float* bias_h = p.bias + ((int64_t)G.type() * p.H + h) * 49 * 64;
+  f32x4 bvs[4][4];
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+      bvs[qt][kt] = *(const f32x4*)(bias_h + (int64_t)min(16 * qt + c16, 48) * 64 + 4 * g + 16 * kt);
   wait_vmcnt0();
 
-  const float* bias_h = p.bias + ((int64_t)G.type(win) * p.H + h) * 49 * 64;
   const int tq = (lane >> 2) & 3, tp = lane & 3;
 #pragma unroll
   for (int qt = 0; qt < 4; ++qt) {
@@ -289,11 +300,10 @@ __global__ __launch_bounds__(256) void window_attn_bf16_kernel(SwinAttnParams p)
     }
     // s[kt][j] = S^T[key 16 kt + 4 g + j][query q]: scores in the log2 domain + bias (incl. the
     // shift mask and -inf past key 49) on packed pairs; max over canonical (computed) values
-    const float* br = bias_h + (int64_t)min(q, 48) * 64 + 4 * g;
     const f32x2 sc2 = {p.scale_log2, p.scale_log2};
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
-      const f32x4 bv = *(const f32x4*)(br + 16 * kt);
+      const f32x4 bv = bvs[qt][kt];
       const f32x2 lo = f32x2{s[kt][0], s[kt][1]} * sc2 + f32x2{bv[0], bv[1]};
       const f32x2 hi = f32x2{s[kt][2], s[kt][3]} * sc2 + f32x2{bv[2], bv[3]};
       s[kt] = f32x4{lo[0], lo[1], hi[0], hi[1]};
@@ -361,24 +371,24 @@ __global__ __launch_bounds__(256) void window_attn_f32_kernel(SwinAttnParams p) 
   const int h = (int)(pair % p.H);
   const int64_t bw = pair / p.H;
   const int win = (int)(bw % nw), b = (int)(bw / nw);
-  const WinGeom G{p.R, p.nwx, p.shift};
+  const WinGeom G(p.R, p.nwx, p.shift, b, win);
   const float* qkv = (const float*)p.qkv;
   float(*Ks)[33] = smem[wave][0];
   float(*Vs)[33] = smem[wave][1];
   for (int e = lane; e < 49 * 32; e += 64) {
     const int t = e >> 5, d = e & 31;
-    const float* rp = qkv + G.row(b, win, t) * p.ldq + h * 32 + d;
+    const float* rp = qkv + G.row(t) * p.ldq + h * 32 + d;
     Ks[t][d] = rp[p.C];
     Vs[t][d] = rp[2 * p.C];
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // wave-private LDS: no barrier
   __builtin_amdgcn_wave_barrier();
   const int t = min(lane, 48);
-  const int64_t qrow = G.row(b, win, t);
+  const int64_t qrow = G.row(t);
   float q[32];
 #pragma unroll
   for (int d = 0; d < 32; ++d) q[d] = qkv[qrow * p.ldq + h * 32 + d];
-  const float* br = p.bias + (((int64_t)G.type(win) * p.H + h) * 49 + t) * 64;
+  const float* br = p.bias + (((int64_t)G.type() * p.H + h) * 49 + t) * 64;
   float sc[49];
   float mx = -INFINITY;
 #pragma unroll
