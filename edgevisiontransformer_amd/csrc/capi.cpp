@@ -989,22 +989,27 @@ int evt_swin_forward(evt_model* m, const float* img, int B, float* logits, void*
       EVT_RC(dense(m, st.merge, c, s));
     }
     for (const SwinBlock& bl : st.blocks) {
-      {  // LN1-folded QKV (+ bias)
+      const bool fuse96 = dt == DT_BF16 && C == 96 && st.H == 3 && gemm_variant() == 0;
+      if (fuse96) {  // stage-1 attention sublayer fused (swin.hip, swin_attn96_kernel)
+        SwinAttnBlockParams ab{m->x, m->xm, m->sx, m->sm, bl.qkv.w, bl.qkv.b, bl.proj.w,
+                               bl.proj.b, bl.bias, bl.qkv.kpad, bl.proj.kpad, B, st.R, bl.shift,
+                               stats_slots(C), m->eps};
+        EVT_HIP(swin_attn96_launch(ab, s), "fused window attention sublayer");
+      }
+      if (!fuse96) {  // LN1-folded QKV (+ bias)
         DenseCall c;
         c.flags = EPI_LNIN | EPI_BIAS;
         c.A = m->x; c.lda = Cst; c.C = m->qkv; c.ldc = 3 * C; c.M = rows; c.N = 3 * C;
         c.stats_in = m->sx; c.ln_width = C;
         EVT_RC(dense(m, bl.qkv, c, s));
-      }
-      SwinAttnParams ap{m->qkv, 3 * C, m->o, Cst, bl.bias, B, st.R, st.R / 7, C, st.H, bl.shift,
-                        scale_log2};
-      EVT_HIP(window_attn_launch(dt, ap, s), "window attention");
-      {  // proj + bias + residual x -> xm (+ stats)
-        DenseCall c;
-        c.flags = EPI_BIAS | EPI_RESID | EPI_STATS;
-        c.A = m->o; c.lda = Cst; c.C = m->xm; c.ldc = Cst; c.M = rows; c.N = Cst;
-        c.resid = m->x; c.ldr = Cst; c.stats_out = m->sm; c.ln_width = C;
-        EVT_RC(dense(m, bl.proj, c, s));
+        SwinAttnParams ap{m->qkv, 3 * C, m->o, Cst, bl.bias, B, st.R, st.R / 7, C, st.H, bl.shift,
+                          scale_log2};
+        EVT_HIP(window_attn_launch(dt, ap, s), "window attention");
+        DenseCall pc;  // proj + bias + residual x -> xm (+ stats)
+        pc.flags = EPI_BIAS | EPI_RESID | EPI_STATS;
+        pc.A = m->o; pc.lda = Cst; pc.C = m->xm; pc.ldc = Cst; pc.M = rows; pc.N = Cst;
+        pc.resid = m->x; pc.ldr = Cst; pc.stats_out = m->sm; pc.ln_width = C;
+        EVT_RC(dense(m, bl.proj, pc, s));
       }
       if (dt == DT_BF16 && C == 96 && st.mlp == 384 && gemm_variant() == 0) {
         // stage-1 MLP (C = 96) fused: hidden kept on chip (swin.hip, swin_mlp96_kernel)

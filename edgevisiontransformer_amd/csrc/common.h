@@ -14,6 +14,7 @@ typedef __attribute__((ext_vector_type(2))) float f32x2;
 typedef __attribute__((ext_vector_type(4))) short i16x4;
 typedef __attribute__((ext_vector_type(8))) short i16x8;
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
 
 #define EVT_LDS __attribute__((address_space(3)))
 

@@ -157,6 +157,24 @@ struct SwinMlpParams {
   float eps;
 };
 hipError_t swin_mlp96_launch(const SwinMlpParams& p, hipStream_t s);
+
+// Fused attention sublayer of a C = 96, 3-head stage (bf16): xm = x + proj(WMSA(LN1(x))) with
+// the cyclic shift, QKV, window attention and proj of one window on chip; + row statistics of xm.
+struct SwinAttnBlockParams {
+  const void* x;           // [B*R*R][96] stage stream (bf16, raster order)
+  void* xm;                // [B*R*R][96] output
+  const float* stats_in;   // [rows][nslots][2] statistics of x (LN1)
+  float* stats_out;        // [rows][nslots][2] statistics of xm
+  const void* wqkv;        // QKV packed [>= 288][ldq] bf16, LN1 gamma folded
+  const float* cqkv;       // [288] beta.W + qkv bias
+  const void* wproj;       // proj packed [>= 96][ldp] bf16
+  const float* bproj;      // [96]
+  const float* bias;       // window bias + mask tables (rpb_dense_launch)
+  int64_t ldq, ldp;
+  int B, R, shift, nslots;
+  float eps;
+};
+hipError_t swin_attn96_launch(const SwinAttnBlockParams& p, hipStream_t s);
 int gemm_variant();  // the process-wide evt_set_gemm_variant value (0 = automatic)
 
 }  // namespace evt

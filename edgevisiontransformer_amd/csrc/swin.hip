@@ -603,6 +603,262 @@ __global__ __launch_bounds__(512, 1) void swin_mlp96_kernel(SwinMlpParams p) {
   }
 }
 
+
+// ---- fused attention sublayer of the C = 96 stage (Swin-T / Swin-S stage 1) --------------------
+// xm = x + proj(WMSA(LN1(x))) for one 7x7 window per block iteration, everything between the x
+// read and the xm write in LDS: the separate QKV GEMM, window attention and proj move 1.7 GB per
+// stage-1 block (qkv 462 MB written + read, o 154 MB written + read, x / xm); here 0.3 GB.
+//   LDS: Wq (QKV, 288 rows x 96 k, LN1 gamma folded) and Wp (proj, 96 x 96), loaded once per
+//   block; per window Xn = LN1(x) of the 49 (64) window tokens (gathered with the cyclic shift),
+//   the window's qkv [64][288] and o [64][96] (bf16).
+//   Phases (8 waves, barriers between): Xn staging; QKV = Wq . Xn^T (+ beta.W + b seeds the
+//   accumulators); 12 (head, query tile) attention units exactly as window_attn_bf16_kernel but
+//   with Q / K / V from LDS; proj = Wp . O^T + b + x (raw rows) -> xm, row statistics.
+constexpr int AT96_ROW = 208;                      // 96-element rows (+ 8 pad)
+constexpr int AT96_QROW = 592;                     // 288-element qkv rows (+ 8 pad)
+constexpr int AT96_WQ = 0;
+constexpr int AT96_WP = AT96_WQ + 288 * AT96_ROW;  // 59904
+constexpr int AT96_XN = AT96_WP + 96 * AT96_ROW;   // 79872
+constexpr int AT96_QKV = AT96_XN + 64 * AT96_ROW;  // 93184
+constexpr int AT96_O = AT96_QKV + 64 * AT96_QROW;  // 131072
+constexpr int AT96_XR = AT96_O + 64 * AT96_ROW;    // 144384: raw x rows (the residual)
+constexpr int AT96_PART = AT96_XR + 64 * AT96_ROW; // 157696
+constexpr int AT96_LDS = AT96_PART + 2 * 64 * 8;   // 158720
+
+__global__ __launch_bounds__(512, 1) void swin_attn96_kernel(SwinAttnBlockParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  EVT_LDS char* L = (EVT_LDS char*)smem;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const bf16* x = (const bf16*)p.x;
+  // ---- weights, once per block ----
+  for (int e = tid; e < 288 * 12; e += 512) {
+    const int n = e / 12, j = e - n * 12;
+    *(EVT_LDS u32x4*)(L + AT96_WQ + n * AT96_ROW + j * 16) =
+        *(const u32x4*)((const bf16*)p.wqkv + (int64_t)n * p.ldq + j * 8);
+  }
+  for (int e = tid; e < 96 * 12; e += 512) {
+    const int n = e / 12, j = e - n * 12;
+    *(EVT_LDS u32x4*)(L + AT96_WP + n * AT96_ROW + j * 16) =
+        *(const u32x4*)((const bf16*)p.wproj + (int64_t)n * p.ldp + j * 8);
+  }
+  const int nwx = p.R / 7, nw = nwx * nwx;
+  const float inv_d = 1.0f / 96.0f;
+  const float scale_log2 = 0.17677669529663687f * kLog2e;
+  // x chunks (token e / 12, 16-B chunk e % 12; e = tid, tid + 512 < 768) and their row
+  // statistics of the NEXT window are loaded during the current window's attention phase
+  u32x4 xc[2];
+  f32x4 sc[2];
+  auto prefetch = [&](int wgn) {
+    const int bn = wgn / nw, wn = wgn - bn * nw;
+    const WinGeom Gn(p.R, nwx, p.shift, bn, wn);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = tid + 512 * k, t = e / 12, j = e - t * 12;
+      xc[k] = u32x4{0u, 0u, 0u, 0u};
+      sc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (e < 768 && t < 49) {
+        const int64_t row = Gn.row(t);
+        xc[k] = *(const u32x4*)(x + row * 96 + j * 8);
+        const float* st = p.stats_in + row * 2 * p.nslots;
+        sc[k] = f32x4{st[0], st[1], p.nslots > 1 ? st[2] : 0.f, p.nslots > 1 ? st[3] : 0.f};
+      }
+    }
+  };
+  if (blockIdx.x < p.B * nw) prefetch(blockIdx.x);
+  f32x4 bpr[3];  // proj bias of this wave's feature tiles (P3), loaded once
+#pragma unroll
+  for (int f = 0; f < 3; ++f) bpr[f] = load4(p.bproj + 16 * ((wave >> 2) * 3 + f) + 4 * g);
+  for (int wg = blockIdx.x; wg < p.B * nw; wg += gridDim.x) {
+    const int b = wg / nw, win = wg - b * nw;
+    const WinGeom G(p.R, nwx, p.shift, b, win);
+    __syncthreads();  // previous window's readers of Xn / XR / QKV / O / part are done
+    // ---- P0: Xn = LN1(x) of the window tokens ((x - mu) r), XR = x (zero rows past 49) ----
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = tid + 512 * k, t = e / 12, j = e - t * 12;
+      if (e >= 768) break;
+      u32x4 nv = u32x4{0u, 0u, 0u, 0u};
+      if (t < 49) {  // (nslots <= 2 here: C = 96)
+        const float s1 = sc[k][0] + sc[k][2], s2 = sc[k][1] + sc[k][3];
+        const float mu = s1 * inv_d;
+        const float r = rsqrtf(fmaxf(s2 * inv_d - mu * mu, 0.f) + p.eps);
+        const bf16x8 xv = __builtin_bit_cast(bf16x8, xc[k]);
+        const f32x2 r2 = {r, r}, o2 = {-mu * r, -mu * r};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x2 f = f32x2{(float)xv[2 * q], (float)xv[2 * q + 1]} * r2 + o2;
+          nv[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(f, bf16x2));
+        }
+      }
+      *(EVT_LDS u32x4*)(L + AT96_XN + t * AT96_ROW + j * 16) = nv;
+      *(EVT_LDS u32x4*)(L + AT96_XR + t * AT96_ROW + j * 16) = xc[k];
+    }
+    __syncthreads();
+    // ---- P1: QKV^T = Wq . Xn^T + cqkv; wave = token tile (wave & 3) x 9 feature tiles ----
+    {
+      const int tt = wave & 3, ft0 = (wave >> 2) * 9;
+      u32x4 bx[3];
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks)
+        bx[ks] = *(const EVT_LDS u32x4*)(L + AT96_XN + (16 * tt + c16) * AT96_ROW + 64 * ks + 16 * g);
+#pragma unroll 3
+      for (int f = 0; f < 9; ++f) {
+        const int ft = ft0 + f;
+        f32x4 acc = load4(p.cqkv + 16 * ft + 4 * g);
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) {
+          const u32x4 wv = *(const EVT_LDS u32x4*)(L + AT96_WQ + (16 * ft + c16) * AT96_ROW + 64 * ks + 16 * g);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wv),
+                                                        __builtin_bit_cast(bf16x8, bx[ks]), acc, 0, 0, 0);
+        }
+        // acc[jj]: feature 16 ft + 4 g + jj, token 16 tt + c16
+        const f32x2 lo = {acc[0], acc[1]}, hi = {acc[2], acc[3]};
+        u32x2 pk = {__builtin_bit_cast(unsigned, __builtin_convertvector(lo, bf16x2)),
+                    __builtin_bit_cast(unsigned, __builtin_convertvector(hi, bf16x2))};
+        *(EVT_LDS u32x2*)(L + AT96_QKV + (16 * tt + c16) * AT96_QROW + (16 * ft + 4 * g) * 2) = pk;
+      }
+    }
+    __syncthreads();
+    // ---- P2: attention, 12 (head, query tile) units over 8 waves (units wave, wave + 8) ----
+    // bias rows of both units first, then the next window's x prefetch: the in-order vmcnt
+    // makes every wait on a load also wait on the loads issued before it
+    f32x4 bvu[2][4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int u = wave + 8 * k;
+      if (u < 12) {
+        const int h = u >> 2, qt = u & 3;
+        const float* br = p.bias + ((int64_t)G.type() * 3 + h) * 49 * 64 +
+                          (int64_t)min(16 * qt + c16, 48) * 64 + 4 * g;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) bvu[k][kt] = *(const f32x4*)(br + 16 * kt);
+      }
+    }
+    if (wg + (int)gridDim.x < p.B * nw) prefetch(wg + gridDim.x);  // lands during P2 / P3
+    const int tq = (lane >> 2) & 3, tp = lane & 3;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int u = wave + 8 * k;
+      if (u >= 12) break;
+      const int h = u >> 2, qt = u & 3;
+      const EVT_LDS char* Q = L + AT96_QKV;
+      const u32x4 qf = *(const EVT_LDS u32x4*)(Q + (16 * qt + c16) * AT96_QROW + (32 * h + 8 * g) * 2);
+      const f32x4* bv = bvu[k];
+      f32x4 sv[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const u32x4 kf = *(const EVT_LDS u32x4*)(Q + (16 * kt + c16) * AT96_QROW + (96 + 32 * h + 8 * g) * 2);
+        sv[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf),
+                                                         __builtin_bit_cast(bf16x8, qf),
+                                                         f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      }
+      const f32x2 sc2 = {scale_log2, scale_log2};
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const f32x2 lo = f32x2{sv[kt][0], sv[kt][1]} * sc2 + f32x2{bv[kt][0], bv[kt][1]};
+        const f32x2 hi = f32x2{sv[kt][2], sv[kt][3]} * sc2 + f32x2{bv[kt][2], bv[kt][3]};
+        sv[kt] = f32x4{lo[0], lo[1], hi[0], hi[1]};
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+        mx = fmaxf(fmaxf(mx, fmaxf(sv[kt][0], sv[kt][1])), fmaxf(sv[kt][2], sv[kt][3]));
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      float sum = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float e = __builtin_amdgcn_exp2f(sv[kt][j] - mx);
+          sv[kt][j] = e;
+          sum += e;
+        }
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 pf;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pf[j] = (bf16)sv[2 * ks][j];
+          pf[4 + j] = (bf16)sv[2 * ks + 1][j];
+        }
+        const int key0 = ks * 32 + 4 * g + tq;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const int col = (192 + 32 * h + 16 * dt + 4 * tp) * 2;
+          const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((EVT_LDS i16x4*)(Q + key0 * AT96_QROW + col));
+          const i16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((EVT_LDS i16x4*)(Q + (key0 + 16) * AT96_QROW + col));
+          const i16x8 vv = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[dt], 0, 0, 0);
+        }
+      }
+      // o[dt][j] = O^T[d = 16 dt + 4 g + j][query 16 qt + c16]
+      const float inv = 1.0f / sum;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const f32x2 lo = f32x2{o[dt][0], o[dt][1]} * f32x2{inv, inv};
+        const f32x2 hi = f32x2{o[dt][2], o[dt][3]} * f32x2{inv, inv};
+        u32x2 pk = {__builtin_bit_cast(unsigned, __builtin_convertvector(lo, bf16x2)),
+                    __builtin_bit_cast(unsigned, __builtin_convertvector(hi, bf16x2))};
+        *(EVT_LDS u32x2*)(L + AT96_O + (16 * qt + c16) * AT96_ROW + (32 * h + 16 * dt + 4 * g) * 2) = pk;
+      }
+    }
+    __syncthreads();
+    // ---- P3: proj + bias + residual -> xm, row statistics (wave = token tile x 3 feature tiles) ----
+    {
+      const int tt = wave & 3, ft0 = (wave >> 2) * 3;
+      u32x4 bo[3];
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks)
+        bo[ks] = *(const EVT_LDS u32x4*)(L + AT96_O + (16 * tt + c16) * AT96_ROW + 64 * ks + 16 * g);
+      const int t = 16 * tt + c16;
+      const bool ok = t < 49;
+      const int64_t row = G.row(min(t, 48));
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int f = 0; f < 3; ++f) {
+        const int ft = ft0 + f;
+        f32x4 acc = bpr[f];
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) {
+          const u32x4 wv = *(const EVT_LDS u32x4*)(L + AT96_WP + (16 * ft + c16) * AT96_ROW + 64 * ks + 16 * g);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wv),
+                                                        __builtin_bit_cast(bf16x8, bo[ks]), acc, 0, 0, 0);
+        }
+        const bf16x4 xr = *(const EVT_LDS bf16x4*)(L + AT96_XR + t * AT96_ROW + (16 * ft + 4 * g) * 2);
+        const f32x4 v = acc + f32x4{(float)xr[0], (float)xr[1], (float)xr[2], (float)xr[3]};
+        const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        if (ok) *(bf16x4*)((bf16*)p.xm + row * 96 + 16 * ft + 4 * g) = o;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const float fv = (float)o[jj];
+          s1 += fv;
+          s2 += fv * fv;
+        }
+      }
+      s1 += __shfl_xor(s1, 16, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (g == 0) *(EVT_LDS f32x2*)(L + AT96_PART + ((wave >> 2) * 64 + t) * 8) = f32x2{s1, s2};
+    }
+    __syncthreads();
+    // ---- P4: row statistics of xm (two partials per token, fixed order) ----
+    if (tid < 49) {
+      const f32x2 a = *(const EVT_LDS f32x2*)(L + AT96_PART + tid * 8);
+      const f32x2 c = *(const EVT_LDS f32x2*)(L + AT96_PART + (64 + tid) * 8);
+      float* so = p.stats_out + G.row(tid) * 2 * p.nslots;
+      so[0] = a[0] + c[0];
+      so[1] = a[1] + c[1];
+      for (int k = 1; k < p.nslots; ++k) so[2 * k] = so[2 * k + 1] = 0.f;
+    }
+  }
+}
+
 template <typename T, int LPR, int NC>
 hipError_t ln_rows_lc(const void* x, int64_t ld, void* y, const float* g, const float* bb,
                       int rows, int D, float eps, float* stats, int nslots, hipStream_t s) {
@@ -710,6 +966,24 @@ hipError_t swin_mlp96_launch(const SwinMlpParams& p, hipStream_t s) {
   const int waves = (p.M + 31) / 32;
   const int grid = std::max(1, std::min(ncu, (waves + 7) / 8));
   hipLaunchKernelGGL(swin_mlp96_kernel, dim3(grid), dim3(512), MLP96_LDS, s, p);
+  return hipGetLastError();
+}
+
+hipError_t swin_attn96_launch(const SwinAttnBlockParams& p, hipStream_t s) {
+  if (p.B <= 0) return hipSuccess;
+  if (p.R % 7 || p.shift < 0 || p.shift >= 7 || p.nslots < 1 || p.nslots > 4 || p.ldq < 96 ||
+      p.ldp < 96 || p.ldq % 8 || p.ldp % 8)
+    return hipErrorInvalidValue;
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipFuncSetAttribute((const void*)swin_attn96_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, AT96_LDS);
+  }
+  const int windows = p.B * (p.R / 7) * (p.R / 7);
+  hipLaunchKernelGGL(swin_attn96_kernel, dim3(std::min(windows, ncu)), dim3(512), AT96_LDS, s, p);
   return hipGetLastError();
 }
 
