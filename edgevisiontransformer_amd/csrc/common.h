@@ -56,20 +56,6 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
-// Exact-form GELU (torch nn.GELU(), the Swin MLP activation): x * Phi(x) = 0.5 x (1 + erf(x/sqrt 2)).
-// erf is evaluated branch-free with Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, below fp32
-// GELU rounding at |x| ~ 1): 0.5 erfc(z) = 0.5 t P(t) exp(-z^2), t = 1 / (1 + 0.3275911 z),
-// z = |x| / sqrt 2; one v_rcp_f32, one v_exp_f32 and 6 FMAs (libm erff is a ranged polynomial
-// with divergent branches: measured 3x slower FC1 epilogues).
-__device__ __forceinline__ float gelu_erf(float x) {
-  const float z = fabsf(x) * 0.7071067811865476f;
-  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * z);
-  const float p = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f +
-                  t * (-1.453152027f + t * 1.061405429f))));
-  const float q = 0.5f * p * __builtin_amdgcn_exp2f(-1.4426950408889634f * z * z);  // 0.5 erfc(z)
-  return x * (x >= 0.f ? 1.0f - q : q);
-}
-
 // Packed-pair forms of the two GELUs (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 for everything but
 // the transcendentals, which have no packed form): the GEMM epilogues are VALU-bound on these.
 __device__ __forceinline__ f32x2 gelu_tanh2(f32x2 x) {
@@ -79,7 +65,9 @@ __device__ __forceinline__ f32x2 gelu_tanh2(f32x2 x) {
   const f32x2 d = f32x2{1.f, 1.f} + f32x2{__builtin_amdgcn_exp2f(u[0]), __builtin_amdgcn_exp2f(u[1])};
   return x * f32x2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
 }
-// A&S 7.1.26 as in gelu_erf, rescaled so that z' = |x| sqrt(log2 e / 2): exp(-x^2/2) = 2^(-z'^2),
+// Exact-form GELU (torch nn.GELU(), the Swin MLP) for the fp32 parity path: x * Phi(x) with erf from
+// Abramowitz & Stegun 7.1.26 (|error| <= 2.1e-7, branch-free; libm erff is a ranged polynomial with
+// divergent branches: measured 3x slower FC1 epilogues), rescaled so that z' = |x| sqrt(log2 e / 2): exp(-x^2/2) = 2^(-z'^2),
 // t = 1 / (1 + p' z') with p' = 0.3275911 / sqrt(log2 e), polynomial coefficients pre-halved (the
 // 0.5 of 0.5 erfc), Phi = 0.5 + copysign(0.5 - q, x).
 __device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
