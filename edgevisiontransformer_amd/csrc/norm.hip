@@ -78,10 +78,29 @@ __global__ __launch_bounds__(256) void patchify_kernel(const float* __restrict__
   __syncthreads();
   const int pd = ps * ps * C;  // patch vector length
   TO* orow = out + ((int64_t)b * np * np + (int64_t)hh * np) * pd;
-  for (int e = tid; e < np * pd; e += 256) {
-    const int ww = e / pd, f = e - ww * pd;
-    const int c = f % C, p12 = f / C, p1 = p12 / ps, p2 = p12 - p1 * ps;
-    orow[(int64_t)ww * pd + f] = from_f32<TO>(strip[c * per_c + p1 * HW + ww * ps + p2]);
+  if (pd % 8 == 0) {
+    // 8 consecutive (p1 p2 c) elements per thread -> one 16-B (bf16) / 2 x 16-B (f32) store; the
+    // strip offsets of a chunk depend only on its position in the patch vector (no per-element
+    // division by the patch index)
+    const int cpp = pd / 8;  // chunks per patch
+    for (int e = tid; e < np * cpp; e += 256) {
+      const int ww = e / cpp, f0 = (e - ww * cpp) * 8;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int f = f0 + j, c = f % C, p12 = f / C, p1 = p12 / ps, p2 = p12 - p1 * ps;
+        v[j] = strip[c * per_c + p1 * HW + ww * ps + p2];
+      }
+      TO* op = orow + (int64_t)ww * pd + f0;
+      store4(op, f32x4{v[0], v[1], v[2], v[3]});
+      store4(op + 4, f32x4{v[4], v[5], v[6], v[7]});
+    }
+  } else {
+    for (int e = tid; e < np * pd; e += 256) {
+      const int ww = e / pd, f = e - ww * pd;
+      const int c = f % C, p12 = f / C, p1 = p12 / ps, p2 = p12 - p1 * ps;
+      orow[(int64_t)ww * pd + f] = from_f32<TO>(strip[c * per_c + p1 * HW + ww * ps + p2]);
+    }
   }
   if (hh == 0 && tid < 64) {  // one wave writes the CLS row and its LayerNorm statistics
     const int64_t row = (int64_t)b * (np * np + 1);
