@@ -19,6 +19,8 @@
 // next 16x16x16 step (bf16: v_mfma_f32_16x16x16_bf16; f32: 4 x v_mfma_f32_16x16x4_f32 over the
 // same k-permutation). Weights live in LDS as [out][in] fp32 rows with the 16-B chunk q of row r
 // stored at q ^ (r & 15) (conflict-free fragment reads).
+#include <type_traits>
+
 #include "common.h"
 #include "evt_internal.h"
 
@@ -433,12 +435,106 @@ __global__ __launch_bounds__(64) void cls_rows_kernel(T* __restrict__ x, int nto
   }
 }
 
+
+// soft_split0 of the fp32 image (k 7, s 4, p 2, C 3: every T2T-ViT, t2t_vit.py:50): one block per
+// (output row oh, image). The 7 input rows the band needs are staged once in LDS with coalesced
+// 16-B loads ([7][W + 2p + pad][3] fp32, zero outside the image: the padding), then every output
+// row (one pixel's 147-vector, zero padded to ldo) leaves as 16-B chunks of 8 elements, 32 lanes
+// per row (ldo / 8 <= 32 chunks); row statistics by shuffles within the 32 lanes. The generic
+// kernel above gathers 4-B elements from 7 image rows per row (1.6 TB/s measured).
+template <typename TO>
+__global__ __launch_bounds__(256) void unfold_k7s4c3_kernel(const float* __restrict__ in, int H,
+                                                            int W, int OW, TO* __restrict__ out,
+                                                            int ldo, float* __restrict__ stats,
+                                                            int nslots) {
+  extern __shared__ __attribute__((aligned(16))) float band[];  // [7][Wp][3]
+  const int oh = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int Wp = W + 8;  // staged columns: iw = -2 .. W + 5 (zero outside [0, W))
+  const int ih0 = oh * 4 - 2;
+  for (int e = tid; e < 7 * Wp; e += 256) {
+    const int kh = e / Wp, cw = e - kh * Wp, ih = ih0 + kh, iw = cw - 2;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f;
+    if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
+      const float* src = in + (((int64_t)b * H + ih) * W + iw) * 3;
+      v0 = src[0];
+      v1 = src[1];
+      v2 = src[2];
+    }
+    float* d = band + (kh * Wp + cw) * 3;
+    d[0] = v0;
+    d[1] = v1;
+    d[2] = v2;
+  }
+  __syncthreads();
+  const int lane = tid & 63, half = lane >> 5, sub = lane & 31, wave = tid >> 6;
+  const int nch = ldo / 8;
+  // this lane's 8 (kh, kw, c) offsets inside a window (relative to the window origin), -1 = pad
+  int off[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = sub * 8 + u;
+    const int kh = e / 21, r = e - kh * 21, kw = r / 3, c = r - kw * 3;
+    off[u] = (sub < nch && e < 147) ? (kh * Wp + kw) * 3 + c : -1;
+  }
+  for (int ow = wave * 2 + half; ow < OW; ow += 8) {
+    const float* win = band + ow * 4 * 3;  // staged column of iw = ow * 4 - 2 is ow * 4
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = off[u] >= 0 ? win[off[u]] : 0.f;
+    const int64_t row = ((int64_t)b * (gridDim.x) + oh) * OW + ow;
+    float s1 = 0.f, s2 = 0.f;
+    if (sub < nch) {
+      TO* op = out + row * ldo + sub * 8;
+      if constexpr (sizeof(TO) == 2) {
+        const bf16x8 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3],
+                          (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
+        *(u32x4*)op = __builtin_bit_cast(u32x4, o);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float q = (float)o[u];
+          s1 += q;
+          s2 += q * q;
+        }
+      } else {
+        store4(op, f32x4{v[0], v[1], v[2], v[3]});
+        store4(op + 4, f32x4{v[4], v[5], v[6], v[7]});
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          s1 += v[u];
+          s2 += v[u] * v[u];
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      s1 += __shfl_xor(s1, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
+    }
+    if (stats && sub < nslots) {
+      float* st = stats + 2 * (row * nslots + sub);
+      st[0] = sub == 0 ? s1 : 0.f;
+      st[1] = sub == 0 ? s2 : 0.f;
+    }
+  }
+}
+
 template <typename TI, typename TO>
 hipError_t unfold_t(const void* in, int B, int H, int W, int C, int k, int s, int p, void* out,
                     int ldo, float* stats, int nslots, hipStream_t st) {
   const int OH = (H + 2 * p - k) / s + 1, OW = (W + 2 * p - k) / s + 1;
   const int64_t rows = (int64_t)B * OH * OW;
   if (rows >= (int64_t)1 << 31) return hipErrorInvalidValue;
+  if constexpr (std::is_same<TI, float>::value) {
+    if (k == 7 && s == 4 && p == 2 && C == 3 && ldo % 8 == 0 && ldo <= 256 && nslots <= 32 &&
+        (OH - 1) * 4 - 2 + 7 <= H + 6) {
+      const size_t lds = (size_t)7 * (W + 8) * 3 * sizeof(float);
+      if (lds <= 64 * 1024) {
+        hipLaunchKernelGGL(unfold_k7s4c3_kernel<TO>, dim3(OH, B), dim3(256), lds, st, (const float*)in,
+                           H, W, OW, (TO*)out, ldo, stats, nslots);
+        return hipGetLastError();
+      }
+    }
+  }
   const int vw = (C % 4 == 0 && ldo % 4 == 0) ? 4 : (ldo % 2 == 0 ? 2 : 1);
   if (ldo > 256 * vw) return hipErrorInvalidValue;  // <= 4 accesses per lane
   const int rpw = 4;

@@ -63,6 +63,31 @@ def test_unfold(gpu, dtype, H, C, k, s, p, in_f32):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("H", [32, 224, 20])
+def test_unfold_soft_split0_padded(gpu, dtype, H):
+    """soft_split0 (k7 s4 p2, C 3) of the fp32 image into 192-wide rows (the model's layout): the
+    LDS-staged kernel; bit-exact values, zero padding columns, row statistics."""
+    k, s_, p_, C, ldo = 7, 4, 2, 3, 192
+    rng = np.random.default_rng(H)
+    x = rng.standard_normal((3, H, H, C)).astype(np.float32)
+    ref = t2t_ref.unfold_nhwc(x.astype(np.float64), k, s_, p_)
+    ref = _round(ref, dtype).reshape(-1, k * k * C)
+    out = torch.full((ref.shape[0], ldo), 7.0, dtype=_ops.TDT[dtype], device=gpu)
+    stats = torch.full((ref.shape[0], 2, 2), 9.0, device=gpu)
+    _lib.check(_lib.load_library().evt_unfold(_lib.DTYPE[dtype], 1, _ops._p(torch.from_numpy(x).to(gpu)),
+                                              3, H, H, C, k, s_, p_, _ops._p(out), ldo,
+                                              _ops._p(stats), 2, _ops._s()))
+    torch.cuda.synchronize()
+    got = out.float().cpu().numpy()
+    np.testing.assert_array_equal(got[:, :147], ref)
+    assert not got[:, 147:].any()
+    st = stats.cpu().numpy().astype(np.float64)
+    np.testing.assert_allclose(st[:, 0, 0], ref.sum(1), rtol=1e-5, atol=1e-4)
+    np.testing.assert_allclose(st[:, 0, 1], (ref * ref).sum(1), rtol=1e-5, atol=1e-4)
+    assert not st[:, 1, :].any()
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
 @pytest.mark.parametrize("T", [784, 3136, 37])
 def test_performer_core(gpu, dtype, T):
     cfg = t2t_config(256, 1, 4, 2)
