@@ -26,6 +26,7 @@ DTYPE = {"f32": 0, "fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1}
 # GEMM epilogue flags (include/evt.h EVT_EPI_*)
 EPI_BIAS, EPI_GELU, EPI_RESID, EPI_POS, EPI_OUT_F32 = 1, 2, 4, 8, 16
 EPI_LNIN, EPI_RESLN, EPI_STATS, EPI_GELU_ERF = 32, 64, 128, 256
+EPI_OUT_MX8 = 512
 SWIN_MAX_STAGES = 8
 
 
@@ -60,6 +61,16 @@ class evt_dense_args(ctypes.Structure):
                 ("rbeta", ctypes.c_void_p), ("stats_out", ctypes.c_void_p),
                 ("ln_width", ctypes.c_int32), ("ln_eps", ctypes.c_float),
                 ("stats_step", ctypes.c_int32)]
+
+
+class evt_dense_mx8_args(ctypes.Structure):
+    _fields_ = [("flags", ctypes.c_int32), ("A", ctypes.c_void_p), ("lda", ctypes.c_int64),
+                ("a_scales", ctypes.c_void_p), ("ld_as", ctypes.c_int64),
+                ("Wq", ctypes.c_void_p), ("Kpad", ctypes.c_int32), ("Npad", ctypes.c_int32),
+                ("w_scales", ctypes.c_void_p), ("C", ctypes.c_void_p), ("ldc", ctypes.c_int64),
+                ("c_scales", ctypes.c_void_p), ("ld_cs", ctypes.c_int64),
+                ("M", ctypes.c_int32), ("N", ctypes.c_int32), ("bias", ctypes.c_void_p),
+                ("resid", ctypes.c_void_p), ("ldr", ctypes.c_int64)]
 
 
 class evt_t2t_desc(ctypes.Structure):
@@ -118,6 +129,9 @@ SIGNATURES = {
                                       ctypes.POINTER(ctypes.c_size_t)]),
     "evt_window_attention": (_I, [_I, _P, _I64, _P, _I64, _P, _I, _I, _I, _I, _I, _P]),
     "evt_patch_merge": (_I, [_I, _P, _I64, _I, _I, _I, _P, _P, _I, _P]),
+    "evt_mx8_quantize": (_I, [_I, _P, _I64, _I, _I, _I, _P, _I64, _P, _I64, _P]),
+    "evt_mx8_pack_weight": (_I, [_P, _P, _I, _I, _P, _I, _I, _P, _P]),
+    "evt_dense_mx8": (_I, [ctypes.POINTER(evt_dense_mx8_args), _P]),
 }
 
 _lib = None

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libevt_hip.so")
 OBJ = os.path.join(HERE, "build_obj")
-SOURCES = ["gemm.hip", "attention.hip", "norm.hip", "t2t.hip", "swin.hip", "capi.cpp"]
+SOURCES = ["gemm.hip", "attention.hip", "norm.hip", "t2t.hip", "swin.hip", "mx8.hip", "capi.cpp"]
 HEADERS = ["common.h", "evt_internal.h", os.path.join("..", "..", "include", "evt.h")]
 ARCH = os.environ.get("EVT_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",

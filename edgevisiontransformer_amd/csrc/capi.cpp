@@ -1099,6 +1099,52 @@ int evt_pack_weight(int dtype, const float* W, const float* row_scale, int K, in
   return EVT_OK;
 }
 
+int evt_mx8_quantize(int in_dtype, const void* x, int64_t ldx, int rows, int K, int Kpad, void* q,
+                     int64_t ldq, uint32_t* scales, int64_t ld_s, void* stream) {
+  if (!x || !q || !scales || rows < 0 || K <= 0 || K % 8 || Kpad < K || Kpad % 128 ||
+      ldx < K || ldq < Kpad || ld_s < rows || ldq % 8 ||
+      (in_dtype != EVT_DTYPE_F32 && in_dtype != EVT_DTYPE_BF16) ||
+      ldx % (in_dtype == EVT_DTYPE_F32 ? 4 : 8))
+    return fail(EVT_EINVAL, "mx8_quantize: bad shape (K % 8, Kpad % 128, aligned rows)");
+  EVT_HIP(mx8_quantize_launch(in_dtype, x, ldx, rows, K, Kpad, q, ldq, scales, ld_s,
+                              (hipStream_t)stream),
+          "mx8_quantize");
+  return EVT_OK;
+}
+
+int evt_mx8_pack_weight(const float* W, const float* row_scale, int K, int N, void* Wq, int Kpad,
+                        int Npad, uint32_t* scales, void* stream) {
+  if (!W || !Wq || !scales || K <= 0 || N <= 0 || Kpad < K || Npad < N || Kpad % 128 ||
+      Npad % 128)
+    return fail(EVT_EINVAL, "mx8_pack: bad shape (Kpad % 128, Npad % 128)");
+  EVT_HIP(mx8_pack_launch(W, row_scale, K, N, Wq, Kpad, Npad, scales, (hipStream_t)stream),
+          "mx8_pack");
+  return EVT_OK;
+}
+
+int evt_dense_mx8(const evt_dense_mx8_args* a, void* stream) {
+  if (!a || !a->A || !a->a_scales || !a->Wq || !a->w_scales || !a->C || a->M < 0 || a->N <= 0 ||
+      a->N % 8 || a->N > a->Npad || a->Kpad <= 0 || a->Kpad % 128 || a->Npad % 128 ||
+      a->lda < a->Kpad || a->lda % 16 || a->ld_as < a->M || a->ldc < a->N || a->ldc % 8)
+    return fail(EVT_EINVAL, "dense_mx8: bad shape (N % 8, Kpad % 128, Npad % 128, lda % 16)");
+  const int f = a->flags;
+  if ((f & EPI_BIAS) && !a->bias) return fail(EVT_EINVAL, "dense_mx8: bias flag without bias");
+  if ((f & EPI_RESID) && (!a->resid || a->ldr < a->N || a->ldr % 8))
+    return fail(EVT_EINVAL, "dense_mx8: bad resid");
+  if ((f & EPI_OUT_MX8) && (!a->c_scales || a->N % 32 || a->ld_cs < a->M))
+    return fail(EVT_EINVAL, "dense_mx8: MX8 output needs c_scales, N % 32, ld_cs >= M");
+  Mx8GemmParams p{};
+  p.A = (const uint8_t*)a->A; p.lda = a->lda; p.As = a->a_scales; p.ldas = a->ld_as;
+  p.W = (const uint8_t*)a->Wq; p.ldw = a->Kpad; p.Ws = a->w_scales; p.ldws = a->Npad;
+  p.C = a->C; p.ldc = a->ldc; p.Cs = a->c_scales; p.ldcs = a->ld_cs;
+  p.M = a->M; p.N = a->N; p.K = a->Kpad;
+  p.bias = a->bias; p.resid = a->resid; p.ldr = a->ldr;
+  hipError_t e = gemm_mx8_launch(f, p, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue) return fail(EVT_EINVAL, "dense_mx8: unsupported flags");
+  EVT_HIP(e, "dense_mx8");
+  return EVT_OK;
+}
+
 int evt_ln_fold(int dtype, const void* Wp, int Kpad, int Npad, const float* W, const float* beta,
                 const float* bias, int K, int N, float* colsum, float* cvec, void* stream) {
   if (!Wp || !W || !beta || !colsum || !cvec || K <= 0 || N <= 0 || Kpad < K || Npad < N)

@@ -19,6 +19,7 @@ enum : int {
   EPI_RESLN = 64,    // residual is LN(resid): (resid - mu_r) * r_r * rgamma[n] + rbeta[n]
   EPI_STATS = 128,   // accumulate (sum, sum of squares) of each output row into stats_out
   EPI_GELU_ERF = 256,  // exact erf GELU (nn.GELU, the Swin MLP)
+  EPI_OUT_MX8 = 512,   // MXFP8 output (mx8.hip GEMM only)
 };
 
 // C[M, N] = epilogue(A[M, K] . W[K, N]) with W pre-packed K-contiguous as Wp[Npad][Kpad].
@@ -176,5 +177,23 @@ struct SwinAttnBlockParams {
 };
 hipError_t swin_attn96_launch(const SwinAttnBlockParams& p, hipStream_t s);
 int gemm_variant();  // the process-wide evt_set_gemm_variant value (0 = automatic)
+
+// ---- MXFP8 (mx8.hip): e4m3fn elements, e8m0 scale per 32 K, scales S[K/128][ld] dwords ----
+struct Mx8GemmParams {
+  const uint8_t* A;  int64_t lda;   // [M][K] e4m3 (bytes)
+  const uint32_t* As; int64_t ldas; // [K/128][ldas] scale dwords (ldas >= M)
+  const uint8_t* W;  int64_t ldw;   // packed [Npad][K] e4m3, Npad multiple of 128
+  const uint32_t* Ws; int64_t ldws; // [K/128][ldws = Npad]
+  void* C;           int64_t ldc;   // bf16 / fp32 / e4m3 bytes (EPI_OUT_MX8)
+  uint32_t* Cs;      int64_t ldcs;  // EPI_OUT_MX8: [N/128][ldcs] output scales (N % 32 == 0)
+  int M, N, K;                      // K multiple of 128, N multiple of 8
+  const float* bias;                // >= N floats
+  const void* resid; int64_t ldr;   // bf16
+};
+hipError_t mx8_quantize_launch(int in_dtype, const void* x, int64_t ldx, int rows, int K, int Kpad,
+                               void* q, int64_t ldq, uint32_t* s, int64_t lds, hipStream_t st);
+hipError_t mx8_pack_launch(const float* W, const float* row_scale, int K, int N, void* Wq, int Kpad,
+                           int Npad, uint32_t* s, hipStream_t st);
+hipError_t gemm_mx8_launch(int flags, const Mx8GemmParams& p, hipStream_t s);
 
 }  // namespace evt

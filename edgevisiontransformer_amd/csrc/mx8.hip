@@ -1,0 +1,372 @@
+// MXFP8 (OCP Microscaling) GEMM, activation quantizer and weight packer for gfx950.
+//
+// The MI355X counterpart of the reference's reduced-precision axis (TFLite float16 / dynamic-range
+// / int8 post-training quantization, `utils.py:242-294`, driven by `tools.py:458-498,826-844`):
+// instead of TFLite's per-tensor int8, the matrix cores' native block-scaled format. A tensor is
+// e4m3fn elements (OCP FP8, max 448) with one e8m0 scale per 32 consecutive K elements:
+//
+//   value(r, k) = e4m3(q[r][k]) * 2^(sbyte(r, k / 32) - 127)
+//
+// Scales are stored k-step-major as dwords S[K / 128][ld_s] (byte j of S[ks][r] = block 4 ks + j of
+// row r), so one GEMM k-step of a 128-row tile reads 512 contiguous bytes of each operand's scales.
+// Quantization follows the OCP MX v1.0 rule: shared exponent = floor(log2(amax)) - 8 (8 = emax of
+// e4m3), elements = RNE(v / 2^e) saturated to +-448; an all-zero block gets scale byte 0.
+//
+// GEMM: v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3, hardware-applied block scales), 2x the
+// bf16 MFMA rate (operand K order and scale lanes measured on the device: scripts/probe/).
+// 128 x 128 tiles, 4 waves (2 x 2) of 64 x 64, K step 128 bytes, operands and
+// scales staged into LDS with global_load_lds (2 stages, 66 KiB: 2 workgroups per CU, so one
+// workgroup's epilogue runs under the other's MFMAs). The product is computed transposed
+// (D^T = W . X^T) with the W rows of each 32-column pair interleaved, so every lane ends with 8
+// consecutive output columns of one row: 16-B bf16 stores, and a 32-column MX block of the output
+// spans exactly the 4 lane groups of one row (2 shuffles for its amax).
+#include "common.h"
+#include "evt_internal.h"
+
+namespace evt {
+
+namespace {
+
+constexpr int MX_BM = 128, MX_BN = 128, MX_BK = 128;  // K step in elements (= bytes)
+constexpr int MX_STAGE = MX_BM * MX_BK + MX_BN * MX_BK + 4 * MX_BM + 4 * MX_BN;  // 33792 B
+
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+// Shared MX scale of a block with absolute maximum amax: the e8m0 byte, and 2^-(e) as fp32.
+__device__ __forceinline__ unsigned mx8_scale_byte(float amax) {
+  const int E = (int)((__float_as_uint(amax) >> 23) & 0xff);  // biased exponent (0: zero/denormal)
+  return (unsigned)max(E - 8, 0);
+}
+__device__ __forceinline__ float mx8_inv_scale(unsigned sb) {  // 2^(127 - sb), sb <= 246
+  return __uint_as_float((254u - sb) << 23);
+}
+// 8 fp32 values (already multiplied by the inverse scale) -> 8 e4m3fn bytes, RNE, saturated.
+__device__ __forceinline__ u32x2 mx8_pack8(const float (&v)[8]) {
+  float c[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) c[i] = __builtin_amdgcn_fmed3f(v[i], -448.f, 448.f);
+  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], lo, true);
+  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(c[4], c[5], 0, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(c[6], c[7], hi, true);
+  return u32x2{(unsigned)lo, (unsigned)hi};
+}
+
+// ---- activation quantizer: rows of K (bf16 / fp32) -> MX8 rows of Kpad ------------------------
+// One lane per 8 elements, 4 lanes per 32-element block (amax over xor-1/2 shuffles).
+template <typename T>
+__global__ __launch_bounds__(256) void mx8_quantize_kernel(const T* __restrict__ x, int64_t ldx,
+                                                           int rows, int K, int Kpad,
+                                                           uint8_t* __restrict__ q, int64_t ldq,
+                                                           uint32_t* __restrict__ s, int64_t lds) {
+  const int chunks = Kpad >> 3;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int r = (int)(t / chunks), c = (int)(t - (int64_t)r * chunks);
+  const bool live = r < rows;
+  float v[8];
+  const int k0 = c * 8;
+  if (live && k0 < K) {
+    const T* p = x + (int64_t)r * ldx + k0;
+    const f32x4 a = load4(p), b = load4(p + 4);
+    v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+    v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0.f;
+  }
+  float am = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) am = fmaxf(am, fabsf(v[i]));
+  am = fmaxf(am, __shfl_xor(am, 1, 64));
+  am = fmaxf(am, __shfl_xor(am, 2, 64));
+  const unsigned sb = mx8_scale_byte(am);
+  const float inv = mx8_inv_scale(sb);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] *= inv;
+  const u32x2 o = mx8_pack8(v);
+  if (!live) return;
+  *(u32x2*)(q + (int64_t)r * ldq + k0) = o;
+  if ((c & 3) == 0) {
+    const int blk = c >> 2;  // 32-element block
+    ((uint8_t*)s)[((int64_t)(blk >> 2) * lds + r) * 4 + (blk & 3)] = (uint8_t)sb;
+  }
+}
+
+// ---- weight packer: Keras W[K][N] fp32 (optionally row-scaled) -> Wq[Npad][Kpad], S[Kpad/128][Npad]
+// One thread per (column n, 32-row block of K); consecutive threads take consecutive n (coalesced
+// reads of the W rows). Padding rows / columns are written as zeros with scale byte 0.
+__global__ __launch_bounds__(256) void mx8_pack_kernel(const float* __restrict__ W,
+                                                       const float* __restrict__ row_scale, int K,
+                                                       int N, uint8_t* __restrict__ Wq, int Kpad,
+                                                       int Npad, uint32_t* __restrict__ s) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int nblk = Kpad >> 5;
+  if (t >= (int64_t)nblk * Npad) return;
+  const int blk = (int)(t / Npad), n = (int)(t - (int64_t)blk * Npad);
+  float v[32];
+  float am = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int k = blk * 32 + i;
+    float w = 0.f;
+    if (n < N && k < K) {
+      w = W[(int64_t)k * N + n];
+      if (row_scale) w *= row_scale[k];
+    }
+    v[i] = w;
+    am = fmaxf(am, fabsf(w));
+  }
+  const unsigned sb = mx8_scale_byte(am);
+  const float inv = mx8_inv_scale(sb);
+  uint8_t* dst = Wq + (int64_t)n * Kpad + blk * 32;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float c[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c[i] = v[8 * j + i] * inv;
+    *(u32x2*)(dst + 8 * j) = mx8_pack8(c);
+  }
+  ((uint8_t*)s)[((int64_t)(blk >> 2) * Npad + n) * 4 + (blk & 3)] = (uint8_t)sb;
+}
+
+// ---- GEMM -----------------------------------------------------------------------------------
+// LDS images are 128-B rows of 16-B chunks, physical chunk = chunk ^ key(row), applied on the glds
+// source address and on every read. ds_read_b128 is serviced in 16-lane groups whose 16 reads must
+// hit distinct (row parity, chunk) slots of the 256-B bank row: X fragments read 16 consecutive
+// rows -> key (row >> 1) & 7; W fragments read rows 8q + s (+ 4h) for l16 = 4q + s -> key
+// 2 ((row >> 3) & 3) + ((row >> 1) & 1). Both conflict-free for the lane groups of the table in
+// MI355X_MICROARCH.md (checked by hand for both 16-B halves of every fragment).
+__device__ __forceinline__ int xkey(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int wkey(int row) { return (((row >> 3) & 3) << 1) | ((row >> 1) & 1); }
+
+template <int FL>
+__global__ __launch_bounds__(256, 2) void gemm_mx8_kernel(Mx8GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4, l16 = lane & 15;
+  const int ntn = (p.N + MX_BN - 1) / MX_BN, ntm = (p.M + MX_BM - 1) / MX_BM;
+  // XCD-aware tile order: the hardware deals consecutive workgroups round-robin over the 8 XCDs,
+  // so give XCD x a contiguous run of tiles (row panels n-fastest: the A panel stays in its L2)
+  int t = blockIdx.x;
+  const int nb = ntm * ntn;
+  if ((nb & 7) == 0) t = (t & 7) * (nb >> 3) + (t >> 3);
+  const int tm = t / ntn, tn = t - tm * ntn;
+  const int m0 = tm * MX_BM, n0 = tn * MX_BN;
+  const int nk = p.K / MX_BK;
+
+  // glds source addresses: 4 wave-instructions per operand per stage, 8 rows of 128 B each
+  const int srow = lane >> 3, spc = lane & 7;
+  const uint8_t* asrc[4];
+  const uint8_t* wsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wave * 4 + i) * 8 + srow;
+    asrc[i] = p.A + (int64_t)min(m0 + row, p.M - 1) * p.lda + (spc ^ xkey(row)) * 16;
+    wsrc[i] = p.W + (int64_t)(n0 + row) * p.ldw + (spc ^ wkey(row)) * 16;
+  }
+  // scales: waves 0 / 1 load the A / W scale dwords of the stage (2 x 64 dwords each)
+  const uint32_t* ssrc0;
+  const uint32_t* ssrc1;
+  if (wave == 0) {
+    ssrc0 = p.As + min(m0 + lane, p.M - 1);
+    ssrc1 = p.As + min(m0 + 64 + lane, p.M - 1);
+  } else {
+    ssrc0 = p.Ws + n0 + lane;
+    ssrc1 = p.Ws + n0 + 64 + lane;
+  }
+  const int64_t sstep = wave == 0 ? p.ldas : p.ldws;
+
+  auto issue = [&](int ks, int buf) {
+    EVT_LDS char* st = (EVT_LDS char*)smem + buf * MX_STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      glds16(asrc[i] + ks * MX_BK, st + (wave * 4 + i) * 8 * MX_BK);
+      glds16(wsrc[i] + ks * MX_BK, st + MX_BM * MX_BK + (wave * 4 + i) * 8 * MX_BK);
+    }
+    if (wave < 2) {
+      EVT_LDS char* sd = st + 2 * MX_BM * MX_BK + wave * 4 * MX_BM;
+      __builtin_amdgcn_global_load_lds(ssrc0 + ks * sstep, sd, 4, 0, 0);
+      __builtin_amdgcn_global_load_lds(ssrc1 + ks * sstep, sd + 256, 4, 0, 0);
+    }
+  };
+
+  // LDS read offsets. X rows (MFMA B operand): wm*64 + mt*16 + l16. W rows (MFMA A operand) of
+  // tile nt = 2 pp + h: wn*64 + pp*32 + 8 (l16 >> 2) + 4 h + (l16 & 3), so that accumulator
+  // register r of lane (l16, g) in tiles 2pp / 2pp+1 is output column pp*32 + 8g + r / + 4 + r.
+  // Lane group g holds k-step bytes [16g, 16g+16) and [64+16g, 64+16g+16) (the hardware K order
+  // of the 16x16x128 operands: block b = bytes [32b, 32b+32) is scaled by lane group b's scale).
+  int xoa[4], xob[4], woa[4], wob[4], xso[4], wso[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int xr = wm * 64 + i * 16 + l16;
+    const int wr = wn * 64 + (i >> 1) * 32 + 8 * (l16 >> 2) + 4 * (i & 1) + (l16 & 3);
+    xoa[i] = xr * MX_BK + ((g ^ xkey(xr)) << 4);
+    xob[i] = xr * MX_BK + (((g + 4) ^ xkey(xr)) << 4);
+    woa[i] = MX_BM * MX_BK + wr * MX_BK + ((g ^ wkey(wr)) << 4);
+    wob[i] = MX_BM * MX_BK + wr * MX_BK + (((g + 4) ^ wkey(wr)) << 4);
+    xso[i] = 2 * MX_BM * MX_BK + xr * 4;
+    wso[i] = 2 * MX_BM * MX_BK + 4 * MX_BM + wr * 4;
+  }
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0, 0);
+  for (int ks = 0; ks < nk; ++ks) {
+    wait_vmcnt0();
+    __syncthreads();
+    if (ks + 1 < nk) issue(ks + 1, (ks + 1) & 1);
+    const EVT_LDS char* st = (const EVT_LDS char*)smem + (ks & 1) * MX_STAGE;
+    i32x8 xf[4], wf[4];
+    int xs[4], ws[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const u32x4 x0 = *(const EVT_LDS u32x4*)(st + xoa[i]);
+      const u32x4 x1 = *(const EVT_LDS u32x4*)(st + xob[i]);
+      const u32x4 w0 = *(const EVT_LDS u32x4*)(st + woa[i]);
+      const u32x4 w1 = *(const EVT_LDS u32x4*)(st + wob[i]);
+      xf[i] = i32x8{(int)x0[0], (int)x0[1], (int)x0[2], (int)x0[3],
+                    (int)x1[0], (int)x1[1], (int)x1[2], (int)x1[3]};
+      wf[i] = i32x8{(int)w0[0], (int)w0[1], (int)w0[2], (int)w0[3],
+                    (int)w1[0], (int)w1[1], (int)w1[2], (int)w1[3]};
+      xs[i] = (int)(*(const EVT_LDS uint32_t*)(st + xso[i]) >> (8 * g));
+      ws[i] = (int)(*(const EVT_LDS uint32_t*)(st + wso[i]) >> (8 * g));
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        acc[nt][mt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+            wf[nt], xf[mt], acc[nt][mt], 0, 0, 0, ws[nt], 0, xs[mt]);
+  }
+
+  // epilogue: lane (l16, g) holds row m = m0 + wm*64 + mt*16 + l16, columns n .. n+7 with
+  // n = n0 + wn*64 + pp*32 + 8g, from acc[2pp][mt] (n..n+3) and acc[2pp+1][mt] (n+4..n+7)
+#pragma unroll
+  for (int pp = 0; pp < 2; ++pp) {
+    const int n = n0 + wn * 64 + pp * 32 + 8 * g;
+    const bool nok = n < p.N;
+    f32x4 b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
+    if ((FL & EPI_BIAS) && nok) {
+      b0 = *(const f32x4*)(p.bias + n);
+      b1 = *(const f32x4*)(p.bias + n + 4);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int m = m0 + wm * 64 + mt * 16 + l16;
+      const bool ok = nok && m < p.M;
+      f32x4 lo = acc[2 * pp][mt], hi = acc[2 * pp + 1][mt];
+      if (FL & EPI_BIAS) {
+        lo += b0;
+        hi += b1;
+      }
+      if (FL & (EPI_GELU | EPI_GELU_ERF)) {
+        const int mode = (FL & EPI_GELU_ERF) ? 2 : 0;
+        lo = gelu4(lo, mode);
+        hi = gelu4(hi, mode);
+      }
+      if ((FL & EPI_RESID) && ok) {
+        const bf16x8 r8 = *(const bf16x8*)((const bf16*)p.resid + (int64_t)m * p.ldr + n);
+        lo += f32x4{(float)r8[0], (float)r8[1], (float)r8[2], (float)r8[3]};
+        hi += f32x4{(float)r8[4], (float)r8[5], (float)r8[6], (float)r8[7]};
+      }
+      if constexpr ((FL & EPI_OUT_MX8) != 0) {
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        float am = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) am = fmaxf(am, fabsf(v[i]));
+        am = fmaxf(am, __shfl_xor(am, 16, 64));
+        am = fmaxf(am, __shfl_xor(am, 32, 64));
+        const unsigned sb = mx8_scale_byte(am);
+        const float inv = mx8_inv_scale(sb);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] *= inv;
+        const u32x2 o = mx8_pack8(v);
+        if (ok) {
+          *(u32x2*)((uint8_t*)p.C + (int64_t)m * p.ldc + n) = o;
+          if (g == 0) {
+            const int blk = n >> 5;
+            ((uint8_t*)p.Cs)[((int64_t)(blk >> 2) * p.ldcs + m) * 4 + (blk & 3)] = (uint8_t)sb;
+          }
+        }
+      } else if constexpr ((FL & EPI_OUT_F32) != 0) {
+        if (ok) {
+          float* c = (float*)p.C + (int64_t)m * p.ldc + n;
+          *(f32x4*)c = lo;
+          *(f32x4*)(c + 4) = hi;
+        }
+      } else {
+        if (ok) {
+          const bf16x8 o = {(bf16)lo[0], (bf16)lo[1], (bf16)lo[2], (bf16)lo[3],
+                            (bf16)hi[0], (bf16)hi[1], (bf16)hi[2], (bf16)hi[3]};
+          *(bf16x8*)((bf16*)p.C + (int64_t)m * p.ldc + n) = o;
+        }
+      }
+    }
+  }
+}
+
+template <int FL>
+hipError_t launch_mx8(const Mx8GemmParams& p, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    attr = true;
+    (void)hipFuncSetAttribute((const void*)gemm_mx8_kernel<FL>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 2 * MX_STAGE);
+  }
+  const int nb = ((p.M + MX_BM - 1) / MX_BM) * ((p.N + MX_BN - 1) / MX_BN);
+  hipLaunchKernelGGL(gemm_mx8_kernel<FL>, dim3(nb), dim3(256), 2 * MX_STAGE, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t mx8_quantize_launch(int in_dtype, const void* x, int64_t ldx, int rows, int K, int Kpad,
+                               void* q, int64_t ldq, uint32_t* s, int64_t lds, hipStream_t st) {
+  if (rows <= 0) return hipSuccess;
+  const int64_t threads = (int64_t)rows * (Kpad >> 3);
+  const dim3 grid((unsigned)((threads + 255) / 256));
+  if (in_dtype == DT_BF16)
+    hipLaunchKernelGGL(mx8_quantize_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)x, ldx,
+                       rows, K, Kpad, (uint8_t*)q, ldq, s, lds);
+  else
+    hipLaunchKernelGGL(mx8_quantize_kernel<float>, grid, dim3(256), 0, st, (const float*)x, ldx,
+                       rows, K, Kpad, (uint8_t*)q, ldq, s, lds);
+  return hipGetLastError();
+}
+
+hipError_t mx8_pack_launch(const float* W, const float* row_scale, int K, int N, void* Wq, int Kpad,
+                           int Npad, uint32_t* s, hipStream_t st) {
+  const int64_t threads = (int64_t)(Kpad >> 5) * Npad;
+  hipLaunchKernelGGL(mx8_pack_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st,
+                     W, row_scale, K, N, (uint8_t*)Wq, Kpad, Npad, s);
+  return hipGetLastError();
+}
+
+hipError_t gemm_mx8_launch(int flags, const Mx8GemmParams& p, hipStream_t s) {
+  if (p.M <= 0) return hipSuccess;
+  switch (flags) {
+    case 0: return launch_mx8<0>(p, s);
+    case EPI_BIAS: return launch_mx8<EPI_BIAS>(p, s);
+    case EPI_BIAS | EPI_GELU: return launch_mx8<EPI_BIAS | EPI_GELU>(p, s);
+    case EPI_BIAS | EPI_GELU_ERF: return launch_mx8<EPI_BIAS | EPI_GELU_ERF>(p, s);
+    case EPI_BIAS | EPI_RESID: return launch_mx8<EPI_BIAS | EPI_RESID>(p, s);
+    case EPI_OUT_F32: return launch_mx8<EPI_OUT_F32>(p, s);
+    case EPI_BIAS | EPI_OUT_F32: return launch_mx8<EPI_BIAS | EPI_OUT_F32>(p, s);
+    case EPI_BIAS | EPI_GELU | EPI_OUT_F32: return launch_mx8<EPI_BIAS | EPI_GELU | EPI_OUT_F32>(p, s);
+    case EPI_BIAS | EPI_GELU_ERF | EPI_OUT_F32:
+      return launch_mx8<EPI_BIAS | EPI_GELU_ERF | EPI_OUT_F32>(p, s);
+    case EPI_OUT_MX8: return launch_mx8<EPI_OUT_MX8>(p, s);
+    case EPI_BIAS | EPI_OUT_MX8: return launch_mx8<EPI_BIAS | EPI_OUT_MX8>(p, s);
+    case EPI_BIAS | EPI_GELU | EPI_OUT_MX8: return launch_mx8<EPI_BIAS | EPI_GELU | EPI_OUT_MX8>(p, s);
+    case EPI_BIAS | EPI_GELU_ERF | EPI_OUT_MX8:
+      return launch_mx8<EPI_BIAS | EPI_GELU_ERF | EPI_OUT_MX8>(p, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace evt

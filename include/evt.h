@@ -311,6 +311,43 @@ int evt_window_attention(int dtype, const void* qkv, int64_t ldq, void* out, int
 int evt_patch_merge(int dtype, const void* x, int64_t ldx, int B, int R, int C, void* out,
                     float* stats, int nslots, void* stream);
 
+/* ---- MXFP8: the reduced-precision axis (reference utils.py:242-294 tf2tflite quantization
+ * 'float16' / 'dynamic' / 'int8', tools.py:458-498) on the MI355X's block-scaled matrix cores.
+ * An MX8 matrix [rows][K] is e4m3fn bytes q[rows][ldq] plus e8m0 scales, one per 32 consecutive K
+ * of a row, stored k-step-major as dwords scales[K/128][ld_s] (ld_s >= rows; byte j of
+ * scales[ks][r] is block 4*ks + j of row r): value = e4m3(q) * 2^(scale - 127). Quantization is
+ * the OCP MX v1.0 rule (shared exponent floor(log2 amax) - 8, RNE, saturate to +-448). */
+#define EVT_EPI_OUT_MX8 512 /* evt_dense_mx8: MX8 output (C bytes + c_scales), N % 32 == 0 */
+
+/* rows x K activations (in_dtype EVT_DTYPE_F32 / _BF16, K % 8 == 0) -> MX8 [rows][Kpad]
+ * (Kpad % 128 == 0, columns past K quantized as zeros). */
+int evt_mx8_quantize(int in_dtype, const void* x, int64_t ldx, int rows, int K, int Kpad, void* q,
+                     int64_t ldq, uint32_t* scales, int64_t ld_s, void* stream);
+
+/* Keras Dense kernel W[K][N] fp32 (optionally row-scaled by row_scale[K]) -> packed MX8 weights
+ * Wq[Npad][Kpad] (row n = output column n, K-contiguous) + scales[Kpad/128][Npad];
+ * Kpad % 128 == 0, Npad % 128 == 0, padding quantized as zeros. */
+int evt_mx8_pack_weight(const float* W, const float* row_scale, int K, int N, void* Wq, int Kpad,
+                        int Npad, uint32_t* scales, void* stream);
+
+typedef struct evt_dense_mx8_args {
+  int32_t flags;                     /* EVT_EPI_BIAS | GELU | GELU_ERF | RESID | OUT_F32 | OUT_MX8 */
+  const void* A; int64_t lda;        /* MX8 [M][Kpad] */
+  const uint32_t* a_scales; int64_t ld_as;
+  const void* Wq; int32_t Kpad; int32_t Npad;
+  const uint32_t* w_scales;          /* [Kpad/128][Npad] */
+  void* C; int64_t ldc;              /* bf16 (default) / fp32 / MX8 bytes */
+  uint32_t* c_scales; int64_t ld_cs; /* EVT_EPI_OUT_MX8 */
+  int32_t M, N;                      /* N % 8 == 0 */
+  const float* bias;
+  const void* resid; int64_t ldr;    /* bf16 */
+} evt_dense_mx8_args;
+
+/* Dense layer on MX8 operands (tf.keras.layers.Dense on the quantized model):
+ * C = epi(dequant(A) . dequant(W)), fp32 accumulation; flag sets 0, 1, 3, 257, 5, 16, 17, 19,
+ * 273, 512, 513, 515, 769. */
+int evt_dense_mx8(const evt_dense_mx8_args* args, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

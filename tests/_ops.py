@@ -90,3 +90,49 @@ def patchify(dtype, img, ps, cls, pos, D):
     _lib.check(_lib.load_library().evt_patchify(_lib.DTYPE[dtype], _p(img), B, C, HW, ps, _p(out),
                                                 _p(x), _p(cls), _p(pos), D, _p(stats), _s()))
     return out, x, stats
+
+
+# ---- MXFP8 (evt_mx8_*) ----
+def mx8_quantize(x: torch.Tensor, Kpad: int = None, ld_s: int = None):
+    """rows x K (bf16 / f32 device tensor) -> (q uint8 [rows, Kpad], scale dwords [Kpad/128, ld_s])."""
+    rows, K = x.shape
+    Kpad = Kpad or round_up(K, 128)
+    ld_s = ld_s or rows
+    q = torch.full((rows, Kpad), 0x7F, dtype=torch.uint8, device=x.device)  # NaN fill: all written
+    s = torch.full((Kpad // 128, ld_s), 0x7F7F7F7F, dtype=torch.int32, device=x.device)
+    dt = 1 if x.dtype == torch.bfloat16 else 0
+    _lib.check(_lib.load_library().evt_mx8_quantize(dt, _p(x), x.stride(0), rows, K, Kpad, _p(q),
+                                                    q.stride(0), _p(s), ld_s, _s()))
+    return q, s
+
+
+def mx8_pack(W: torch.Tensor, row_scale: torch.Tensor = None):
+    K, N = W.shape
+    kpad, npad = round_up(K, 128), round_up(N, 128)
+    wq = torch.full((npad, kpad), 0x7F, dtype=torch.uint8, device=W.device)
+    s = torch.full((kpad // 128, npad), 0x7F7F7F7F, dtype=torch.int32, device=W.device)
+    _lib.check(_lib.load_library().evt_mx8_pack_weight(_p(W.contiguous()), _p(row_scale), K, N,
+                                                       _p(wq), kpad, npad, _p(s), _s()))
+    return wq, s, kpad, npad
+
+
+def dense_mx8(flags, Aq, As, wq, ws, kpad, npad, M, N, bias=None, resid=None):
+    a = _lib.evt_dense_mx8_args()
+    a.flags, a.A, a.lda, a.a_scales, a.ld_as = flags, Aq.data_ptr(), Aq.stride(0), As.data_ptr(), As.shape[1]
+    a.Wq, a.Kpad, a.Npad, a.w_scales = wq.data_ptr(), kpad, npad, ws.data_ptr()
+    a.M, a.N = M, N
+    Cs = None
+    if flags & _lib.EPI_OUT_MX8:
+        C = torch.full((M, N), 0x7F, dtype=torch.uint8, device=Aq.device)
+        Cs = torch.full((N // 128 if N % 128 == 0 else N // 128 + 1, M), 0x7F7F7F7F,
+                        dtype=torch.int32, device=Aq.device)
+        a.c_scales, a.ld_cs = Cs.data_ptr(), M
+    else:
+        C = torch.zeros((M, N), dtype=torch.float32 if flags & _lib.EPI_OUT_F32 else torch.bfloat16,
+                        device=Aq.device)
+    a.C, a.ldc = C.data_ptr(), C.stride(0)
+    a.bias = bias.data_ptr() if bias is not None else None
+    a.resid = resid.data_ptr() if resid is not None else None
+    a.ldr = resid.stride(0) if resid is not None else 0
+    _lib.check(_lib.load_library().evt_dense_mx8(ctypes.byref(a), _s()))
+    return (C, Cs) if Cs is not None else C
