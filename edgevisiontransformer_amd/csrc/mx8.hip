@@ -14,9 +14,10 @@
 //
 // GEMM: v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3, hardware-applied block scales), 2x the
 // bf16 MFMA rate (operand K order and scale lanes measured on the device: scripts/probe/).
-// 128 x 128 tiles, 4 waves (2 x 2) of 64 x 64, K step 128 bytes, operands and
-// scales staged into LDS with global_load_lds (2 stages, 66 KiB: 2 workgroups per CU, so one
-// workgroup's epilogue runs under the other's MFMAs). The product is computed transposed
+// Persistent 128 x 256 tiles, 8 waves (2 x 4) of 64 x 64, K step 128 bytes, operands and
+// scales staged into LDS with global_load_lds in a 3-stage pipeline (148.5 KiB, one workgroup
+// per CU, two stages in flight under every k-step; 128 x 128 tiles with 2 stages and 2
+// workgroups per CU measured 755 TF/s on the DeiT QKV shape: load-latency bound). The product is computed transposed
 // (D^T = W . X^T) with the W rows of each 32-column pair interleaved, so every lane ends with 8
 // consecutive output columns of one row: 16-B bf16 stores, and a 32-column MX block of the output
 // spans exactly the 4 lane groups of one row (2 shuffles for its amax).
@@ -27,8 +28,9 @@ namespace evt {
 
 namespace {
 
-constexpr int MX_BM = 128, MX_BN = 128, MX_BK = 128;  // K step in elements (= bytes)
-constexpr int MX_STAGE = MX_BM * MX_BK + MX_BN * MX_BK + 4 * MX_BM + 4 * MX_BN;  // 33792 B
+constexpr int MX_BM = 128, MX_BN = 256, MX_BK = 128;  // K step in elements (= bytes)
+constexpr int MX_STAGE = MX_BM * MX_BK + MX_BN * MX_BK + 4 * MX_BM + 4 * MX_BN;  // 50688 B
+constexpr int MX_NSTAGE = 3;                                                    // 148.5 KiB
 
 typedef __attribute__((ext_vector_type(8))) int i32x8;
 
@@ -139,113 +141,12 @@ __global__ __launch_bounds__(256) void mx8_pack_kernel(const float* __restrict__
 __device__ __forceinline__ int xkey(int row) { return (row >> 1) & 7; }
 __device__ __forceinline__ int wkey(int row) { return (((row >> 3) & 3) << 1) | ((row >> 1) & 1); }
 
+// Epilogue of one tile: lane (l16, g) of wave (wm, wn) holds row m = m0 + wm*64 + mt*16 + l16,
+// columns n .. n+7 with n = n0 + wn*64 + pp*32 + 8g, from acc[2pp][mt] (n..n+3) and
+// acc[2pp+1][mt] (n+4..n+7).
 template <int FL>
-__global__ __launch_bounds__(256, 2) void gemm_mx8_kernel(Mx8GemmParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int g = lane >> 4, l16 = lane & 15;
-  const int ntn = (p.N + MX_BN - 1) / MX_BN, ntm = (p.M + MX_BM - 1) / MX_BM;
-  // XCD-aware tile order: the hardware deals consecutive workgroups round-robin over the 8 XCDs,
-  // so give XCD x a contiguous run of tiles (row panels n-fastest: the A panel stays in its L2)
-  int t = blockIdx.x;
-  const int nb = ntm * ntn;
-  if ((nb & 7) == 0) t = (t & 7) * (nb >> 3) + (t >> 3);
-  const int tm = t / ntn, tn = t - tm * ntn;
-  const int m0 = tm * MX_BM, n0 = tn * MX_BN;
-  const int nk = p.K / MX_BK;
-
-  // glds source addresses: 4 wave-instructions per operand per stage, 8 rows of 128 B each
-  const int srow = lane >> 3, spc = lane & 7;
-  const uint8_t* asrc[4];
-  const uint8_t* wsrc[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = (wave * 4 + i) * 8 + srow;
-    asrc[i] = p.A + (int64_t)min(m0 + row, p.M - 1) * p.lda + (spc ^ xkey(row)) * 16;
-    wsrc[i] = p.W + (int64_t)(n0 + row) * p.ldw + (spc ^ wkey(row)) * 16;
-  }
-  // scales: waves 0 / 1 load the A / W scale dwords of the stage (2 x 64 dwords each)
-  const uint32_t* ssrc0;
-  const uint32_t* ssrc1;
-  if (wave == 0) {
-    ssrc0 = p.As + min(m0 + lane, p.M - 1);
-    ssrc1 = p.As + min(m0 + 64 + lane, p.M - 1);
-  } else {
-    ssrc0 = p.Ws + n0 + lane;
-    ssrc1 = p.Ws + n0 + 64 + lane;
-  }
-  const int64_t sstep = wave == 0 ? p.ldas : p.ldws;
-
-  auto issue = [&](int ks, int buf) {
-    EVT_LDS char* st = (EVT_LDS char*)smem + buf * MX_STAGE;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      glds16(asrc[i] + ks * MX_BK, st + (wave * 4 + i) * 8 * MX_BK);
-      glds16(wsrc[i] + ks * MX_BK, st + MX_BM * MX_BK + (wave * 4 + i) * 8 * MX_BK);
-    }
-    if (wave < 2) {
-      EVT_LDS char* sd = st + 2 * MX_BM * MX_BK + wave * 4 * MX_BM;
-      __builtin_amdgcn_global_load_lds(ssrc0 + ks * sstep, sd, 4, 0, 0);
-      __builtin_amdgcn_global_load_lds(ssrc1 + ks * sstep, sd + 256, 4, 0, 0);
-    }
-  };
-
-  // LDS read offsets. X rows (MFMA B operand): wm*64 + mt*16 + l16. W rows (MFMA A operand) of
-  // tile nt = 2 pp + h: wn*64 + pp*32 + 8 (l16 >> 2) + 4 h + (l16 & 3), so that accumulator
-  // register r of lane (l16, g) in tiles 2pp / 2pp+1 is output column pp*32 + 8g + r / + 4 + r.
-  // Lane group g holds k-step bytes [16g, 16g+16) and [64+16g, 64+16g+16) (the hardware K order
-  // of the 16x16x128 operands: block b = bytes [32b, 32b+32) is scaled by lane group b's scale).
-  int xoa[4], xob[4], woa[4], wob[4], xso[4], wso[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int xr = wm * 64 + i * 16 + l16;
-    const int wr = wn * 64 + (i >> 1) * 32 + 8 * (l16 >> 2) + 4 * (i & 1) + (l16 & 3);
-    xoa[i] = xr * MX_BK + ((g ^ xkey(xr)) << 4);
-    xob[i] = xr * MX_BK + (((g + 4) ^ xkey(xr)) << 4);
-    woa[i] = MX_BM * MX_BK + wr * MX_BK + ((g ^ wkey(wr)) << 4);
-    wob[i] = MX_BM * MX_BK + wr * MX_BK + (((g + 4) ^ wkey(wr)) << 4);
-    xso[i] = 2 * MX_BM * MX_BK + xr * 4;
-    wso[i] = 2 * MX_BM * MX_BK + 4 * MX_BM + wr * 4;
-  }
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  issue(0, 0);
-  for (int ks = 0; ks < nk; ++ks) {
-    wait_vmcnt0();
-    __syncthreads();
-    if (ks + 1 < nk) issue(ks + 1, (ks + 1) & 1);
-    const EVT_LDS char* st = (const EVT_LDS char*)smem + (ks & 1) * MX_STAGE;
-    i32x8 xf[4], wf[4];
-    int xs[4], ws[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const u32x4 x0 = *(const EVT_LDS u32x4*)(st + xoa[i]);
-      const u32x4 x1 = *(const EVT_LDS u32x4*)(st + xob[i]);
-      const u32x4 w0 = *(const EVT_LDS u32x4*)(st + woa[i]);
-      const u32x4 w1 = *(const EVT_LDS u32x4*)(st + wob[i]);
-      xf[i] = i32x8{(int)x0[0], (int)x0[1], (int)x0[2], (int)x0[3],
-                    (int)x1[0], (int)x1[1], (int)x1[2], (int)x1[3]};
-      wf[i] = i32x8{(int)w0[0], (int)w0[1], (int)w0[2], (int)w0[3],
-                    (int)w1[0], (int)w1[1], (int)w1[2], (int)w1[3]};
-      xs[i] = (int)(*(const EVT_LDS uint32_t*)(st + xso[i]) >> (8 * g));
-      ws[i] = (int)(*(const EVT_LDS uint32_t*)(st + wso[i]) >> (8 * g));
-    }
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        acc[nt][mt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-            wf[nt], xf[mt], acc[nt][mt], 0, 0, 0, ws[nt], 0, xs[mt]);
-  }
-
-  // epilogue: lane (l16, g) holds row m = m0 + wm*64 + mt*16 + l16, columns n .. n+7 with
-  // n = n0 + wn*64 + pp*32 + 8g, from acc[2pp][mt] (n..n+3) and acc[2pp+1][mt] (n+4..n+7)
+__device__ __forceinline__ void mx8_epilogue(const Mx8GemmParams& p, const f32x4 (&acc)[4][4],
+                                             int m0, int n0, int wm, int wn, int g, int l16) {
 #pragma unroll
   for (int pp = 0; pp < 2; ++pp) {
     const int n = n0 + wn * 64 + pp * 32 + 8 * g;
@@ -310,16 +211,173 @@ __global__ __launch_bounds__(256, 2) void gemm_mx8_kernel(Mx8GemmParams p) {
   }
 }
 
+// Persistent: one 8-wave workgroup per CU walks the tiles u = blockIdx + j * gridDim
+// (XCD-remapped); the (tile, k-step) sequence is one flat 3-stage glds pipeline (two stages in
+// flight during every k-step's MFMAs, and the next tile's first stages during the epilogue).
+template <int FL>
+__global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(Mx8GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int g = lane >> 4, l16 = lane & 15;
+  const int ntn = (p.N + MX_BN - 1) / MX_BN, ntm = (p.M + MX_BM - 1) / MX_BM;
+  const int nb = ntm * ntn, nk = p.K / MX_BK;
+  const int b = blockIdx.x, grid = gridDim.x;
+  const int mine = b < nb ? (nb - 1 - b) / grid + 1 : 0;
+  const int total = mine * nk;
+  // XCD-aware tile order: workgroup b runs on XCD b % 8 (grid is a multiple of 8), so give XCD x
+  // a contiguous run of tiles (row panels n-fastest: the A panel stays in its L2)
+  // (the first nb & ~7 tiles are dealt out; a tail of < 8 tiles keeps its index)
+  const int nb8 = nb & ~7;
+  auto tile_of = [&](int j) {
+    int u = b + j * grid;
+    if ((grid & 7) == 0 && u < nb8) u = (u & 7) * (nb8 >> 3) + (u >> 3);
+    return u;
+  };
+
+  // glds: per stage 16 A and 32 W wave-instructions of 8 rows x 128 B (2 + 4 per wave), the
+  // swizzle on the per-lane source chunk; scale dwords by waves 0 (A, 2 x 64) and 1-2 (W, 4 x 64)
+  const int srow = lane >> 3, spc = lane & 7;
+  int arow[2], ach[2], wrow[4], wch[4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    arow[i] = (wave * 2 + i) * 8 + srow;
+    ach[i] = (spc ^ xkey(arow[i])) * 16;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    wrow[i] = (wave * 4 + i) * 8 + srow;
+    wch[i] = (spc ^ wkey(wrow[i])) * 16;
+  }
+  auto issue = [&](int s) {
+    const int j = s / nk, ks = s - j * nk;
+    const int t = tile_of(j);
+    const int tm = t / ntn, m0 = tm * MX_BM, n0 = (t - tm * ntn) * MX_BN;
+    EVT_LDS char* st = (EVT_LDS char*)smem + (s % MX_NSTAGE) * MX_STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      glds16(p.A + (int64_t)min(m0 + arow[i], p.M - 1) * p.lda + ks * MX_BK + ach[i],
+             st + (wave * 2 + i) * 8 * MX_BK);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      glds16(p.W + (int64_t)min(n0 + wrow[i], (int)p.ldws - 1) * p.ldw + ks * MX_BK + wch[i],
+             st + MX_BM * MX_BK + (wave * 4 + i) * 8 * MX_BK);
+    EVT_LDS char* sd = st + (MX_BM + MX_BN) * MX_BK;
+    if (wave == 0) {
+      const uint32_t* src = p.As + (int64_t)ks * p.ldas;
+      __builtin_amdgcn_global_load_lds(src + min(m0 + lane, p.M - 1), sd, 4, 0, 0);
+      __builtin_amdgcn_global_load_lds(src + min(m0 + 64 + lane, p.M - 1), sd + 256, 4, 0, 0);
+    } else if (wave <= 2) {
+      // (tiles past the packed width, Npad = ldws a multiple of 128 only: rows clamped)
+      const uint32_t* src = p.Ws + (int64_t)ks * p.ldws;
+      const int c0 = n0 + (wave - 1) * 128 + lane, last = (int)p.ldws - 1;
+      EVT_LDS char* wd = sd + 4 * MX_BM + (wave - 1) * 512;
+      __builtin_amdgcn_global_load_lds(src + min(c0, last), wd, 4, 0, 0);
+      __builtin_amdgcn_global_load_lds(src + min(c0 + 64, last), wd + 256, 4, 0, 0);
+    }
+  };
+
+  // Lane group g holds k-step bytes [16g, 16g+16) and [64+16g, 64+16g+16) (the hardware K order
+  // of the 16x16x128 operands: block b = bytes [32b, 32b+32) is scaled by lane group b's scale).
+  // X rows (MFMA B operand): wm*64 + mt*16 + l16. W rows (MFMA A operand) of tile nt = 2 pp + h:
+  // wn*64 + pp*32 + 8 (l16 >> 2) + 4 h + (l16 & 3), so that accumulator register r of lane
+  // (l16, g) in tiles 2pp / 2pp+1 is output column pp*32 + 8g + r / + 4 + r.
+  int xoa[4], xob[4], woa[4], wob[4], xso[4], wso[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int xr = wm * 64 + i * 16 + l16;
+    const int wr = wn * 64 + (i >> 1) * 32 + 8 * (l16 >> 2) + 4 * (i & 1) + (l16 & 3);
+    xoa[i] = xr * MX_BK + ((g ^ xkey(xr)) << 4);
+    xob[i] = xr * MX_BK + (((g + 4) ^ xkey(xr)) << 4);
+    woa[i] = MX_BM * MX_BK + wr * MX_BK + ((g ^ wkey(wr)) << 4);
+    wob[i] = MX_BM * MX_BK + wr * MX_BK + (((g + 4) ^ wkey(wr)) << 4);
+    xso[i] = (MX_BM + MX_BN) * MX_BK + xr * 4;
+    wso[i] = (MX_BM + MX_BN) * MX_BK + 4 * MX_BM + wr * 4;
+  }
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (total == 0) return;
+  issue(0);
+  if (total > 1) issue(1);
+  int ks = 0, j = 0;
+  bool drained = false;  // an epilogue's stores sit behind the prefetch: wait for everything
+  for (int s = 0; s < total; ++s) {
+    // stage s complete; stage s+1 (issued last iteration) may stay in flight: the vector memory
+    // counter retires in order, so vmcnt(#loads of one stage) suffices unless an epilogue's
+    // (data-dependent) stores were issued behind it
+    if (drained || s + 1 >= total) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (wave <= 2) {
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    }
+    // a bare s_barrier (__syncthreads' fence would drain the prefetch stage with vmcnt(0))
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + 2 < total) issue(s + 2);
+    drained = false;
+    const EVT_LDS char* st = (const EVT_LDS char*)smem + (s % MX_NSTAGE) * MX_STAGE;
+    i32x8 xf[4], wf[4];
+    int xs[4], ws[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const u32x4 x0 = *(const EVT_LDS u32x4*)(st + xoa[i]);
+      const u32x4 x1 = *(const EVT_LDS u32x4*)(st + xob[i]);
+      const u32x4 w0 = *(const EVT_LDS u32x4*)(st + woa[i]);
+      const u32x4 w1 = *(const EVT_LDS u32x4*)(st + wob[i]);
+      xf[i] = i32x8{(int)x0[0], (int)x0[1], (int)x0[2], (int)x0[3],
+                    (int)x1[0], (int)x1[1], (int)x1[2], (int)x1[3]};
+      wf[i] = i32x8{(int)w0[0], (int)w0[1], (int)w0[2], (int)w0[3],
+                    (int)w1[0], (int)w1[1], (int)w1[2], (int)w1[3]};
+      xs[i] = (int)(*(const EVT_LDS uint32_t*)(st + xso[i]) >> (8 * g));
+      ws[i] = (int)(*(const EVT_LDS uint32_t*)(st + wso[i]) >> (8 * g));
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        acc[nt][mt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+            wf[nt], xf[mt], acc[nt][mt], 0, 0, 0, ws[nt], 0, xs[mt]);
+    if (++ks == nk) {
+      const int t = tile_of(j);
+      const int tm = t / ntn;
+      mx8_epilogue<FL>(p, acc, tm * MX_BM, (t - tm * ntn) * MX_BN, wm, wn, g, l16);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ks = 0;
+      ++j;
+      drained = true;
+    }
+  }
+}
+
 template <int FL>
 hipError_t launch_mx8(const Mx8GemmParams& p, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
     attr = true;
     (void)hipFuncSetAttribute((const void*)gemm_mx8_kernel<FL>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 2 * MX_STAGE);
+                        hipFuncAttributeMaxDynamicSharedMemorySize, MX_NSTAGE * MX_STAGE);
+  }
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
   }
   const int nb = ((p.M + MX_BM - 1) / MX_BM) * ((p.N + MX_BN - 1) / MX_BN);
-  hipLaunchKernelGGL(gemm_mx8_kernel<FL>, dim3(nb), dim3(256), 2 * MX_STAGE, s, p);
+  const int grid = min(nb, cus);  // one resident 8-wave workgroup per CU (148.5 KiB of LDS)
+  hipLaunchKernelGGL(gemm_mx8_kernel<FL>, dim3(grid), dim3(512), MX_NSTAGE * MX_STAGE, s, p);
   return hipGetLastError();
 }
 

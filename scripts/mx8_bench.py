@@ -29,12 +29,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rows", type=int, default=512 * 197)
+    ap.add_argument("--only", default="", help="comma list of gemm names (qkv,proj,fc1,fc2)")
+    ap.add_argument("--no-bf16", action="store_true")
     a = ap.parse_args()
     _lib.ensure_device(0)
     dev = torch.device("cuda", 0)
     M = a.rows
     shapes = [("qkv", 768, 2304, 1, 1), ("proj", 768, 768, 5, 1), ("fc1", 768, 3072, 515, 3),
               ("fc2", 3072, 768, 5, 1)]
+    if a.only:
+        shapes = [x for x in shapes if x[0] in a.only.split(",")]
     for name, K, N, fmx, fbf in shapes:
         g = torch.Generator(device=dev).manual_seed(K + N)
         x = torch.randn((M, K), device=dev, generator=g)
@@ -48,7 +52,7 @@ def main():
         xb = x.to(torch.bfloat16)
         wp, kp, np_ = _ops.pack(W, "bf16")
         C = torch.empty((M, N), dtype=torch.bfloat16, device=dev)
-        t_bf = timeit(lambda: _ops.dense("bf16", fbf, xb, wp, kp, np_, M, N, bias=bias,
+        t_bf = 1e30 if a.no_bf16 else timeit(lambda: _ops.dense("bf16", fbf, xb, wp, kp, np_, M, N, bias=bias,
                                          resid=resid if fbf & 4 else None, C=C), a.reps)
         t_q = timeit(lambda: _ops.mx8_quantize(x.to(torch.bfloat16) if False else xb), a.reps)
         fl = 2.0 * M * K * N
