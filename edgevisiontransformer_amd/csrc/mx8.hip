@@ -213,7 +213,7 @@ __device__ __forceinline__ void mx8_epilogue(const Mx8GemmParams& p, const f32x4
 
 // Persistent: one 8-wave workgroup per CU walks the tiles u = blockIdx + j * gridDim
 // (XCD-remapped); the (tile, k-step) sequence is one flat 3-stage glds pipeline (two stages in
-// flight during every k-step's MFMAs, and the next tile's first stages during the epilogue).
+// flight during every k-step's MFMAs, the next tile's first stage during the epilogue).
 template <int FL>
 __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(Mx8GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -305,12 +305,12 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(Mx8GemmParams p) {
   issue(0);
   if (total > 1) issue(1);
   int ks = 0, j = 0;
-  bool drained = false;  // an epilogue's stores sit behind the prefetch: wait for everything
   for (int s = 0; s < total; ++s) {
-    // stage s complete; stage s+1 (issued last iteration) may stay in flight: the vector memory
-    // counter retires in order, so vmcnt(#loads of one stage) suffices unless an epilogue's
-    // (data-dependent) stores were issued behind it
-    if (drained || s + 1 >= total) {
+    // stage s complete; stage s+1 may stay in flight. The vector memory counter retires in order
+    // and stage s+1 is always the youngest group issued (a tile's epilogue runs BEFORE the next
+    // prefetch is issued), so vmcnt(#loads of one stage) also covers the epilogue's loads and
+    // stores, whatever their data-dependent count.
+    if (s + 1 >= total) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if (wave <= 2) {
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -321,8 +321,8 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(Mx8GemmParams p) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (s + 2 < total) issue(s + 2);
-    drained = false;
+    const bool tile_end = ks + 1 == nk;
+    if (!tile_end && s + 2 < total) issue(s + 2);
     const EVT_LDS char* st = (const EVT_LDS char*)smem + (s % MX_NSTAGE) * MX_STAGE;
     i32x8 xf[4], wf[4];
     int xs[4], ws[4];
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(Mx8GemmParams p) {
       for (int mt = 0; mt < 4; ++mt)
         acc[nt][mt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
             wf[nt], xf[mt], acc[nt][mt], 0, 0, 0, ws[nt], 0, xs[mt]);
-    if (++ks == nk) {
+    if (tile_end) {
       const int t = tile_of(j);
       const int tm = t / ntn;
       mx8_epilogue<FL>(p, acc, tm * MX_BM, (t - tm * ntn) * MX_BN, wm, wn, g, l16);
@@ -353,9 +353,11 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(Mx8GemmParams p) {
       for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (s + 2 < total) issue(s + 2);
       ks = 0;
       ++j;
-      drained = true;
+    } else {
+      ++ks;
     }
   }
 }

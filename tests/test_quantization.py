@@ -1,0 +1,65 @@
+"""MX8Dense (edgevisiontransformer_amd.quantization): argument validation on the CPU; on the GPU,
+the layer against the MX oracle on its own quantized operands, and a quantized FeedForward
+(ffn.py:8-9: Dense(M, gelu) -> Dense(D), FC1 re-quantized in its epilogue) against the fp64
+float FeedForward (accuracy of the MXFP8 path: cosine >= 0.999 per row)."""
+import numpy as np
+import pytest
+import torch
+
+from edgevisiontransformer_amd import quantization as q
+from oracle import mx8_ref
+
+
+def test_validation_before_device():
+    with pytest.raises(ValueError):
+        q.MX8Dense(torch.zeros(4), None)
+    with pytest.raises(ValueError):
+        q.MX8Dense(torch.zeros(64, 64), None, activation="relu")
+    with pytest.raises(ValueError):
+        q.MX8Dense(torch.zeros(64, 60), None)
+
+
+def _gelu(x):
+    return 0.5 * x * (1.0 + np.tanh(np.sqrt(2.0 / np.pi) * (x + 0.044715 * x ** 3)))
+
+
+@pytest.mark.gpu
+def test_mx8_dense_matches_oracle(gpu):
+    g = np.random.default_rng(0)
+    M, K, N = 300, 384, 1536
+    x = g.standard_normal((M, K)).astype(np.float32)
+    W = (g.standard_normal((K, N)) / np.sqrt(K)).astype(np.float32)
+    b = (0.1 * g.standard_normal(N)).astype(np.float32)
+    layer = q.MX8Dense(torch.from_numpy(W), torch.from_numpy(b), activation="gelu", device=gpu)
+    xt = torch.from_numpy(x).to(gpu).to(torch.bfloat16)
+    xq = q.quantize_mx8(xt)
+    y = layer(xq, out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    aq = xq.q.cpu().numpy()
+    asb = mx8_ref.dwords_to_scales(xq.scales.cpu().numpy().view(np.uint32), M)
+    wsb = mx8_ref.dwords_to_scales(layer.ws.cpu().numpy().view(np.uint32), layer.npad)
+    ref = mx8_ref.dense_mx8(aq, asb, layer.wq.cpu().numpy(), wsb, N, 3, bias=b)
+    mag = np.abs(mx8_ref.dequantize(aq, asb)) @ np.abs(mx8_ref.dequantize(layer.wq.cpu().numpy(), wsb)[:N]).T
+    assert np.all(np.abs(y.cpu().numpy() - ref) <= 3e-5 * mag + 1e-6 * np.abs(ref) + 1e-6)
+
+
+@pytest.mark.gpu
+def test_mx8_feedforward_accuracy(gpu):
+    g = np.random.default_rng(1)
+    M, D, F = 197 * 2, 768, 3072
+    x = g.standard_normal((M, D)).astype(np.float32)
+    W1 = (g.standard_normal((D, F)) / np.sqrt(D)).astype(np.float32)
+    b1 = (0.02 * g.standard_normal(F)).astype(np.float32)
+    W2 = (g.standard_normal((F, D)) / np.sqrt(F)).astype(np.float32)
+    b2 = (0.02 * g.standard_normal(D)).astype(np.float32)
+    fc1 = q.MX8Dense(torch.from_numpy(W1), torch.from_numpy(b1), activation="gelu", device=gpu)
+    fc2 = q.MX8Dense(torch.from_numpy(W2), torch.from_numpy(b2), device=gpu)
+    xt = torch.from_numpy(x).to(gpu).to(torch.bfloat16)
+    y = fc2(fc1.quantized_output(xt), residual=xt)
+    torch.cuda.synchronize()
+    xb = xt.float().cpu().numpy().astype(np.float64)
+    ref = _gelu(xb @ W1 + b1) @ W2 + b2 + xb
+    got = y.float().cpu().numpy()
+    cos = (got * ref).sum(1) / np.linalg.norm(got, axis=1) / np.linalg.norm(ref, axis=1)
+    assert cos.min() >= 0.999, cos.min()
+    assert np.abs(got - ref).max() <= 0.05 * np.abs(ref).max()
