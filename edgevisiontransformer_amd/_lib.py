@@ -21,7 +21,7 @@ EVT_EINVAL = -22
 EVT_ENOMEM = -12
 EVT_EHIP = -5
 EVT_ENODEV = -19
-DTYPE = {"f32": 0, "fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1}
+DTYPE = {"f32": 0, "fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1, "mx8": 2}
 
 # GEMM epilogue flags (include/evt.h EVT_EPI_*)
 EPI_BIAS, EPI_GELU, EPI_RESID, EPI_POS, EPI_OUT_F32 = 1, 2, 4, 8, 16

@@ -63,10 +63,18 @@ struct DenseW {  // packed Dense layer
   int K = 0, N = 0, kpad = 0, npad = 0;
 };
 
+struct Mx8W {  // MXFP8-packed Dense layer (mx8.hip): Wq [npad][kpad] e4m3, scales [kpad/128][npad]
+  void* w = nullptr;
+  uint32_t* s = nullptr;
+  float* b = nullptr;       // [npad] fp32 bias, zero padded (zeros for the bias-less QKV)
+  int K = 0, N = 0, kpad = 0, npad = 0;
+};
+
 struct Layer {
   int heads = 0, inner = 0, ffn = 0, ffn_st = 0;
   float *ln1_g = nullptr, *ln1_b = nullptr, *ln2_g = nullptr, *ln2_b = nullptr;
   DenseW qkv, out, fc1, fc2;
+  Mx8W mqkv, mout, mfc1, mfc2;  // EVT_DTYPE_MX8 models
 };
 
 struct Shape {
@@ -96,6 +104,13 @@ struct SwinStage {
 struct evt_model {
   int family = 0;            // 0: ViT / ViT_Pruned, 1: T2T-ViT, 2: Swin
   bool standard = false;     // ViT with EVT_VIT_STANDARD semantics
+  bool mx8 = false;          // EVT_DTYPE_MX8: MXFP8 encoder Dense layers (dtype is then bf16)
+  void* qa = nullptr;        // MX8: [rows][max(Dpad, innerpad)] e4m3 A operand (LN out / attn out)
+  uint32_t* sa = nullptr;    // MX8: its scales [pad/128][rows]
+  void* qh = nullptr;        // MX8: [rows][ffnpad] FC1 output (e4m3, zero-initialised)
+  uint32_t* shd = nullptr;   // MX8: its scales
+  void* ybuf = nullptr;      // MX8: [rows][D] bf16 LayerNorm output (the block's residual)
+  int qa_ld = 0, qh_ld = 0;
   float eps = 1e-5f;         // LayerNorm epsilon of every folded LayerNorm
   int dtype = 0, D = 0, max_batch = 0, num_classes = 0;
   evt_vit_desc desc{};       // ViT only
@@ -149,8 +164,10 @@ int dev_alloc(evt_model* m, void** p, size_t bytes) {
 
 int validate(const evt_vit_desc* d, Shape* sh) {
   if (!d) return fail(EVT_EINVAL, "desc is NULL");
-  if (d->dtype != EVT_DTYPE_F32 && d->dtype != EVT_DTYPE_BF16)
-    return fail(EVT_EINVAL, "dtype must be EVT_DTYPE_F32 or EVT_DTYPE_BF16");
+  if (d->dtype != EVT_DTYPE_F32 && d->dtype != EVT_DTYPE_BF16 && d->dtype != EVT_DTYPE_MX8)
+    return fail(EVT_EINVAL, "dtype must be EVT_DTYPE_F32, EVT_DTYPE_BF16 or EVT_DTYPE_MX8");
+  if (d->dtype == EVT_DTYPE_MX8 && d->semantics != EVT_VIT_REFERENCE)
+    return fail(EVT_EINVAL, "EVT_DTYPE_MX8 supports EVT_VIT_REFERENCE semantics only");
   if (d->patch_size <= 0 || d->image_size <= 0 || d->image_size % d->patch_size != 0)
     return fail(EVT_EINVAL, "image dimensions must be divisible by the patch size");
   if (d->in_chans <= 0 || d->num_classes <= 0 || d->depth < 0 || d->mlp_dim <= 0)
@@ -219,13 +236,53 @@ int copy_vec(evt_model* m, float** dst, const float* src, size_t n, hipStream_t 
   return EVT_OK;
 }
 
+// Pack a Keras [K, N] Dense kernel to MXFP8 (no LayerNorm folding: the MX8 model normalises in
+// the quantizer). N is padded to 32 columns of zeros so an MX8 output covers whole blocks.
+int make_mx8(evt_model* m, Mx8W* dw, const float* W, const float* bias, int K, int N,
+             hipStream_t s) {
+  dw->K = K;
+  dw->N = (int)round_up(N, 32);
+  dw->kpad = (int)round_up(K, 128);
+  dw->npad = (int)round_up(N, 128);
+  EVT_RC(dev_alloc(m, &dw->w, (size_t)dw->kpad * dw->npad));
+  EVT_RC(dev_alloc(m, (void**)&dw->s, (size_t)dw->kpad / 128 * dw->npad * 4));
+  EVT_HIP(mx8_pack_launch(W, nullptr, K, N, dw->w, dw->kpad, dw->npad, dw->s, s), "mx8_pack");
+  EVT_RC(dev_alloc(m, (void**)&dw->b, (size_t)dw->npad * sizeof(float)));
+  EVT_HIP(hipMemsetAsync(dw->b, 0, (size_t)dw->npad * sizeof(float), s), "memset bias");
+  if (bias)
+    EVT_HIP(hipMemcpyAsync(dw->b, bias, (size_t)N * sizeof(float), hipMemcpyDeviceToDevice, s),
+            "copy bias");
+  return EVT_OK;
+}
+
+int dense_mx8(const Mx8W& w, int flags, const void* A, int64_t lda, const uint32_t* as, void* C,
+              int64_t ldc, uint32_t* cs, int M, const void* resid, int64_t ldr, hipStream_t s) {
+  Mx8GemmParams p{};
+  p.A = (const uint8_t*)A; p.lda = lda; p.As = as; p.ldas = M;
+  p.W = (const uint8_t*)w.w; p.ldw = w.kpad; p.Ws = w.s; p.ldws = w.npad;
+  p.C = C; p.ldc = ldc; p.Cs = cs; p.ldcs = M;
+  p.M = M; p.N = w.N; p.K = w.kpad;
+  p.bias = w.b; p.resid = resid; p.ldr = ldr;
+  EVT_HIP(gemm_mx8_launch(flags, p, s), "dense_mx8");
+  return EVT_OK;
+}
+
 size_t workspace_bytes(const evt_vit_desc* d, const Shape& sh, int B) {
-  const size_t es = elem_size(d->dtype);
+  const bool mx8 = d->dtype == EVT_DTYPE_MX8;
+  const size_t es = elem_size(mx8 ? DT_BF16 : d->dtype);
   const size_t rows = (size_t)B * sh.T;
   const size_t hb = std::max(rows * sh.max_ffn_st, (size_t)B * sh.P * sh.pd) * es;
+  size_t extra = 0;
+  if (mx8) {  // qa + sa, qh + its scales, ybuf (run_encoder_mx8)
+    const size_t qa = std::max(round_up(sh.D, 128), round_up(sh.max_inner, 128));
+    int maxffn = 0;
+    for (int i = 0; i < d->depth; ++i) maxffn = std::max(maxffn, (int)d->ffn[i]);
+    const size_t qh = round_up(maxffn, 128);
+    extra = rows * (qa + qa / 32 + qh + qh / 32 + 2 * sh.D) + 5 * 256;
+  }
   return 2 * rows * sh.D * es + 2 * rows * stats_slots(sh.D) * 2 * sizeof(float) +
          rows * 3 * sh.max_inner * es +
-         rows * sh.max_inner * es + hb + (size_t)B * sh.head_st * es + 9 * 256;
+         rows * sh.max_inner * es + hb + (size_t)B * sh.head_st * es + 9 * 256 + extra;
 }
 
 struct DenseCall {
@@ -305,6 +362,16 @@ int build_encoder(evt_model* m, const float* const* w, hipStream_t s) {
     L.ffn_st = (int)round_up(L.ffn, PAD_N);
     EVT_RC(copy_vec(m, &L.ln1_g, w[k + 0], D, s));
     EVT_RC(copy_vec(m, &L.ln1_b, w[k + 1], D, s));
+    if (m->mx8) {  // reference semantics only (validate): no qkv bias
+      EVT_RC(copy_vec(m, &L.ln2_g, w[k + 5], D, s));
+      EVT_RC(copy_vec(m, &L.ln2_b, w[k + 6], D, s));
+      EVT_RC(make_mx8(m, &L.mqkv, w[k + 2], nullptr, D, 3 * L.inner, s));
+      EVT_RC(make_mx8(m, &L.mout, w[k + 3], w[k + 4], L.inner, D, s));
+      EVT_RC(make_mx8(m, &L.mfc1, w[k + 7], w[k + 8], D, L.ffn, s));
+      EVT_RC(make_mx8(m, &L.mfc2, w[k + 9], w[k + 10], L.ffn, D, s));
+      k += 11;
+      continue;
+    }
     EVT_RC(make_dense(m, &L.qkv, w[k + 2], qb ? w[k + 3] : nullptr, D, 3 * L.inner, s, w[k + 0],
                       w[k + 1]));
     k += qb;
@@ -377,6 +444,36 @@ int run_encoder(evt_model* m, int B, hipStream_t s) {
       c.stats_out = m->sx;
       EVT_RC(dense(m, L.fc2, c, s));
     }
+  }
+  return EVT_OK;
+}
+
+// MX8 encoder (reference semantics, transformer_encoder.py:13-18): per sublayer the LayerNorm
+// runs in the quantizer (y = LN(x) kept in bf16 as the residual, norm.py:11-12 + residual.py:9),
+// the Dense layers on the block-scaled MFMA, FC1's GELU output re-quantized in its epilogue.
+int run_encoder_mx8(evt_model* m, int B, hipStream_t s) {
+  const int D = m->D, T = m->sh.T, rows = B * T;
+  const float log2e = 1.4426950408889634f;
+  const int dpad = (int)round_up(D, 128);
+  for (const Layer& L : m->layers) {
+    EVT_HIP(ln_mx8_launch(m->x, rows, D, dpad, L.ln1_g, L.ln1_b, m->eps, m->ybuf, m->qa, m->sa, s),
+            "ln1 mx8");
+    EVT_RC(dense_mx8(L.mqkv, EPI_BIAS, m->qa, dpad, m->sa, m->qkv, 3 * L.inner, nullptr, rows,
+                     nullptr, 0, s));
+    AttnParams ap{m->qkv, 3 * L.inner, m->o, L.inner, T, L.heads, B, 0.125f * log2e};
+    EVT_HIP(attention_launch(DT_BF16, ap, s), "attention");
+    const int ipad = L.mout.kpad;
+    EVT_HIP(mx8_quantize_launch(DT_BF16, m->o, L.inner, rows, L.inner, ipad, m->qa, ipad, m->sa,
+                                rows, s),
+            "quantize attn out");
+    EVT_RC(dense_mx8(L.mout, EPI_BIAS | EPI_RESID, m->qa, ipad, m->sa, m->xm, D, nullptr, rows,
+                     m->ybuf, D, s));
+    EVT_HIP(ln_mx8_launch(m->xm, rows, D, dpad, L.ln2_g, L.ln2_b, m->eps, m->ybuf, m->qa, m->sa, s),
+            "ln2 mx8");
+    EVT_RC(dense_mx8(L.mfc1, EPI_BIAS | EPI_GELU | EPI_OUT_MX8, m->qa, dpad, m->sa, m->qh,
+                     m->qh_ld, m->shd, rows, nullptr, 0, s));
+    EVT_RC(dense_mx8(L.mfc2, EPI_BIAS | EPI_RESID, m->qh, m->qh_ld, m->shd, m->x, D, nullptr,
+                     rows, m->ybuf, D, s));
   }
   return EVT_OK;
 }
@@ -585,7 +682,8 @@ int evt_vit_create(const evt_vit_desc* desc, const float* const* w, int n_weight
   hipStream_t s = (hipStream_t)stream;
   evt_model* m = new evt_model();
   m->family = 0;
-  m->dtype = desc->dtype;
+  m->mx8 = desc->dtype == EVT_DTYPE_MX8;
+  m->dtype = m->mx8 ? DT_BF16 : desc->dtype;  // MX8 models keep bf16 for everything else
   m->D = desc->dim;
   m->max_batch = desc->max_batch;
   m->num_classes = desc->num_classes;
@@ -614,11 +712,26 @@ int evt_vit_create(const evt_vit_desc* desc, const float* const* w, int n_weight
       EVT_RC(make_dense(m, &m->head2, w[k + 2], w[k + 3], desc->mlp_dim, desc->num_classes, s));
     }
     const int B = desc->max_batch;
-    const size_t es = elem_size(desc->dtype);
+    const size_t es = elem_size(m->dtype);
     EVT_RC(alloc_encoder_ws(m, B, std::max((size_t)B * sh.T * sh.max_ffn_st,
                                            (size_t)B * sh.P * sh.pd) * es, s));
     m->apatch = m->hbuf;
     EVT_RC(dev_alloc(m, &m->hh, (size_t)B * sh.head_st * es));
+    if (m->mx8) {
+      const size_t rows = (size_t)B * sh.T;
+      m->qa_ld = (int)std::max(round_up(D, 128), round_up(sh.max_inner, 128));
+      int maxffn = 0;
+      for (int f : m->ffn) maxffn = std::max(maxffn, f);
+      m->qh_ld = (int)round_up(maxffn, 128);
+      EVT_RC(dev_alloc(m, &m->qa, rows * m->qa_ld));
+      EVT_RC(dev_alloc(m, (void**)&m->sa, rows * (m->qa_ld / 128) * 4));
+      EVT_RC(dev_alloc(m, &m->qh, rows * m->qh_ld));
+      EVT_RC(dev_alloc(m, (void**)&m->shd, rows * (m->qh_ld / 128) * 4));
+      EVT_RC(dev_alloc(m, &m->ybuf, rows * D * 2));
+      // FC1 writes columns < roundup(ffn, 32) only: the rest of the FC2 operand stays zero
+      EVT_HIP(hipMemsetAsync(m->qh, 0, rows * m->qh_ld, s), "memset qh");
+      EVT_HIP(hipMemsetAsync(m->shd, 0, rows * (m->qh_ld / 128) * 4, s), "memset qh scales");
+    }
     m->ws_bytes = workspace_bytes(desc, sh, B);
     EVT_HIP(hipStreamSynchronize(s), "create sync");
     return EVT_OK;
@@ -634,7 +747,7 @@ int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* 
   hipStream_t s = (hipStream_t)stream;
   const evt_vit_desc& d = m->desc;
   const Shape& sh = m->sh;
-  const int D = d.dim, T = sh.T, dt = d.dtype;
+  const int D = d.dim, T = sh.T, dt = m->dtype;
   // patch embedding (vit.py:45-51): rearrange -> Dense(D) + pos, CLS row = cls + pos[0]
   EVT_HIP(patchify_launch(dt, img, B, d.in_chans, d.image_size, d.patch_size, m->apatch, m->x,
                           m->cls, m->pos, D, m->sx, s),
@@ -646,7 +759,7 @@ int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* 
     c.pos = m->pos; c.ldp = D; c.P = sh.P; c.stats_out = m->sx;
     EVT_RC(dense(m, m->patch, c, s));
   }
-  EVT_RC(run_encoder(m, B, s));
+  EVT_RC(m->mx8 ? run_encoder_mx8(m, B, s) : run_encoder(m, B, s));
   if (m->standard) {  // final LayerNorm of the CLS rows folded into the Linear head
     DenseCall c;
     c.flags = EPI_LNIN | EPI_BIAS | EPI_OUT_F32;

@@ -195,5 +195,10 @@ hipError_t mx8_quantize_launch(int in_dtype, const void* x, int64_t ldx, int row
 hipError_t mx8_pack_launch(const float* W, const float* row_scale, int K, int N, void* Wq, int Kpad,
                            int Npad, uint32_t* s, hipStream_t st);
 hipError_t gemm_mx8_launch(int flags, const Mx8GemmParams& p, hipStream_t s);
+// LayerNorm of bf16 rows [rows][D] -> y bf16 [rows][D] (if y) and MX8 q [rows][Kpad] +
+// scales [Kpad/128][rows]; D % 8 == 0, D <= Kpad <= 1024.
+hipError_t ln_mx8_launch(const void* x, int rows, int D, int Kpad, const float* gamma,
+                         const float* beta, float eps, void* y, void* q, uint32_t* s,
+                         hipStream_t st);
 
 }  // namespace evt

@@ -94,6 +94,93 @@ __global__ __launch_bounds__(256) void mx8_quantize_kernel(const T* __restrict__
   }
 }
 
+// ---- LayerNorm + MX8 quantization of a bf16 token stream (the MX8 model's LN1 / LN2) --------
+// One wave per row: y = (x - mu) * rsqrt(var + eps) * gamma + beta (population variance, Keras
+// LayerNormalization, reference norm.py:6), written as bf16 (the reference block's residual is
+// LN(x), norm.py:11-12) when y != null, and as MX8 [Kpad] (columns past D quantized as zeros).
+// Lane l owns 8-element chunks l, l + 64 (D <= 1024); 4 consecutive chunks = one MX block.
+__global__ __launch_bounds__(256) void ln_mx8_kernel(const bf16* __restrict__ x, int rows, int D,
+                                                     int Kpad, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps,
+                                                     bf16* __restrict__ y, uint8_t* __restrict__ q,
+                                                     uint32_t* __restrict__ s) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;  // wave-uniform
+  const int nch = D >> 3, nq = Kpad >> 3;
+  const bf16* xr = x + (int64_t)r * D;
+  float v[2][8];
+  float sum = 0.f;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int c = lane + 64 * it;
+    if (c < nch) {
+      const bf16x8 b = *(const bf16x8*)(xr + 8 * c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[it][e] = (float)b[e];
+        sum += v[it][e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[it][e] = 0.f;
+    }
+  }
+  const float mu = wave_sum(sum) / (float)D;
+  float sq = 0.f;
+#pragma unroll
+  for (int it = 0; it < 2; ++it)
+    if (lane + 64 * it < nch)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = v[it][e] - mu;
+        sq += d * d;
+      }
+  const float rstd = rsqrtf(wave_sum(sq) / (float)D + eps);
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int c = lane + 64 * it;
+    if (64 * it >= nq) break;  // wave-uniform: no chunk of this pass is in the padded row
+    const bool live = c < nch;
+    if (live) {
+      const f32x4 g0 = *(const f32x4*)(gamma + 8 * c), g1 = *(const f32x4*)(gamma + 8 * c + 4);
+      const f32x4 b0 = *(const f32x4*)(beta + 8 * c), b1 = *(const f32x4*)(beta + 8 * c + 4);
+      const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+      const float bb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[it][e] = (v[it][e] - mu) * rstd * gg[e] + bb[e];
+      if (y) {
+        const bf16x8 o = {(bf16)v[it][0], (bf16)v[it][1], (bf16)v[it][2], (bf16)v[it][3],
+                          (bf16)v[it][4], (bf16)v[it][5], (bf16)v[it][6], (bf16)v[it][7]};
+        *(bf16x8*)(y + (int64_t)r * D + 8 * c) = o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[it][e] = (float)o[e];  // quantize what the residual holds
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[it][e] = 0.f;
+    }
+    float am = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf(v[it][e]));
+    am = fmaxf(am, __shfl_xor(am, 1, 64));
+    am = fmaxf(am, __shfl_xor(am, 2, 64));
+    const unsigned sb = mx8_scale_byte(am);
+    const float inv = mx8_inv_scale(sb);
+    float t[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t[e] = v[it][e] * inv;
+    const u32x2 o8 = mx8_pack8(t);
+    if (c < nq) {
+      *(u32x2*)(q + (int64_t)r * Kpad + 8 * c) = o8;
+      if ((c & 3) == 0) {
+        const int blk = c >> 2;
+        ((uint8_t*)s)[((int64_t)(blk >> 2) * rows + r) * 4 + (blk & 3)] = (uint8_t)sb;
+      }
+    }
+  }
+}
+
 // ---- weight packer: Keras W[K][N] fp32 (optionally row-scaled) -> Wq[Npad][Kpad], S[Kpad/128][Npad]
 // One thread per (column n, 32-row block of K); consecutive threads take consecutive n (coalesced
 // reads of the W rows). Padding rows / columns are written as zeros with scale byte 0.
@@ -396,6 +483,16 @@ hipError_t mx8_quantize_launch(int in_dtype, const void* x, int64_t ldx, int row
   else
     hipLaunchKernelGGL(mx8_quantize_kernel<float>, grid, dim3(256), 0, st, (const float*)x, ldx,
                        rows, K, Kpad, (uint8_t*)q, ldq, s, lds);
+  return hipGetLastError();
+}
+
+hipError_t ln_mx8_launch(const void* x, int rows, int D, int Kpad, const float* gamma,
+                         const float* beta, float eps, void* y, void* q, uint32_t* s,
+                         hipStream_t st) {
+  if (rows <= 0) return hipSuccess;
+  if (D % 8 || D > 1024 || Kpad % 128 || Kpad < D || Kpad > 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ln_mx8_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, (const bf16*)x, rows,
+                     D, Kpad, gamma, beta, eps, (bf16*)y, (uint8_t*)q, s);
   return hipGetLastError();
 }
 

@@ -39,6 +39,9 @@ extern "C" {
 
 #define EVT_DTYPE_F32 0  /* exact fp32 path (v_mfma_f32_16x16x4_f32), logits within 1e-3 */
 #define EVT_DTYPE_BF16 1 /* bf16 MFMA, fp32 accumulate / LN / softmax / GELU statistics */
+#define EVT_DTYPE_MX8 2  /* evt_vit_* with EVT_VIT_REFERENCE only: MXFP8 (OCP MX e4m3) encoder
+                          * Dense layers (QKV, out-proj, FC1, FC2) on the block-scaled MFMA,
+                          * LayerNorm in the quantizer, bf16 patch embed / attention / head */
 
 /* Static shape of a ViT / ViT_Pruned (reference modeling/models/vit.py:11-75).
  * heads/head_dim/ffn are per-layer arrays of length `depth` (the pruned encoding, decoded by the
