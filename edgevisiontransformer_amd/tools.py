@@ -124,7 +124,8 @@ def _server_flags(parser: argparse.ArgumentParser) -> None:
     parser.add_argument("--num_runs", type=int, default=50)
     parser.add_argument("--warmup_runs", type=int, default=50)
     parser.add_argument("--dtype", default="float32", type=str, help="input data type (float32)")
-    parser.add_argument("--compute_dtype", default="bf16", choices=["bf16", "f32"])
+    parser.add_argument("--compute_dtype", default="bf16", choices=["bf16", "f32", "mx8"],
+                        help="mx8: MXFP8 encoder Dense layers (ViT family; the quantization axis)")
     parser.add_argument("--intra_op_threads", type=int, default=1, help="accepted; unused")
     parser.add_argument("--top", type=int, default=None,
                         help="number of shortest runs to take average")
@@ -159,7 +160,8 @@ def test_keras_latency(argv: Optional[List[str]] = None) -> str:
     parser.add_argument("--use_gpu", action="store_true")
     parser.add_argument("--test_times", type=int, default=5)
     parser.add_argument("--input_shape", required=True, type=str)
-    parser.add_argument("--compute_dtype", default="bf16", choices=["bf16", "f32"])
+    parser.add_argument("--compute_dtype", default="bf16", choices=["bf16", "f32", "mx8"],
+                        help="mx8: MXFP8 encoder Dense layers (ViT family; the quantization axis)")
     args = parser.parse_args(argv)
     shape = _input_shape(args.model, args.input_shape)
     model = build_model(args.model, args.compute_dtype, max_batch=shape[0])
@@ -196,7 +198,8 @@ def prune_benchmark(argv: Optional[List[str]] = None) -> List[str]:
     parser.add_argument("--warmup_runs", type=int, default=10)
     parser.add_argument("--top", type=int, default=None)
     parser.add_argument("--precision", default=2, choices=[2, 3, 4, 5, 6], type=int)
-    parser.add_argument("--compute_dtype", default="bf16", choices=["bf16", "f32"])
+    parser.add_argument("--compute_dtype", default="bf16", choices=["bf16", "f32", "mx8"],
+                        help="mx8: MXFP8 encoder Dense layers (ViT family; the quantization axis)")
     parser.add_argument("--io_binding", action="store_true")
     args = parser.parse_args(argv)
     lines = []
