@@ -107,3 +107,25 @@ def test_swin_host_validation(lib):
     assert b"head size" in lib.evt_last_error()
     d.num_heads[0], d.image_size = 3, 192  # 48 -> stage resolutions not multiples of 7
     assert lib.evt_swin_query_workspace(ctypes.byref(d), 256, ctypes.byref(out)) == _lib.EVT_EINVAL
+
+
+def test_mx8_dtype_host_validation(lib):
+    """EVT_DTYPE_MX8 (2): accepted for the reference semantics, workspace includes the MX8
+    operand buffers (qa, qh, their scales, the bf16 LayerNorm output); rejected for STANDARD."""
+    from edgevisiontransformer_amd import _lib
+    arr = (ctypes.c_int32 * 12)(*([12] * 12))
+    hd = (ctypes.c_int32 * 12)(*([64] * 12))
+    ffn = (ctypes.c_int32 * 12)(*([3072] * 12))
+    out_bf, out_8 = ctypes.c_size_t(), ctypes.c_size_t()
+    d = _lib.evt_vit_desc(224, 16, 3, 1000, 768, 12, 3072, arr, hd, ffn, 1, 512)
+    assert lib.evt_query_workspace(ctypes.byref(d), 512, ctypes.byref(out_bf)) == 0
+    d8 = _lib.evt_vit_desc(224, 16, 3, 1000, 768, 12, 3072, arr, hd, ffn, 2, 512)
+    assert lib.evt_query_workspace(ctypes.byref(d8), 512, ctypes.byref(out_8)) == 0
+    rows = 512 * 197
+    extra = rows * (768 + 768 // 32 + 3072 + 3072 // 32 + 2 * 768)
+    assert out_8.value - out_bf.value >= extra
+    d8.semantics = _lib.VIT_STANDARD
+    assert lib.evt_query_workspace(ctypes.byref(d8), 512, ctypes.byref(out_8)) == _lib.EVT_EINVAL
+    assert b"MX8" in lib.evt_last_error()
+    d8.semantics, d8.dtype = _lib.VIT_REFERENCE, 3
+    assert lib.evt_query_workspace(ctypes.byref(d8), 512, ctypes.byref(out_8)) == _lib.EVT_EINVAL
