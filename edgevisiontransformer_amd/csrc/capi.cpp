@@ -109,7 +109,7 @@ struct evt_model {
   uint32_t* sa = nullptr;    // MX8: its scales [pad/128][rows]
   void* qh = nullptr;        // MX8: [rows][ffnpad] FC1 output (e4m3, zero-initialised)
   uint32_t* shd = nullptr;   // MX8: its scales
-  void* ybuf = nullptr;      // MX8: [rows][D] bf16 LayerNorm output (the block's residual)
+  float* lnst = nullptr;     // MX8: [rows][2] (mu, rstd) of the last LayerNorm'd rows
   int qa_ld = 0, qh_ld = 0;
   float eps = 1e-5f;         // LayerNorm epsilon of every folded LayerNorm
   int dtype = 0, D = 0, max_batch = 0, num_classes = 0;
@@ -256,13 +256,16 @@ int make_mx8(evt_model* m, Mx8W* dw, const float* W, const float* bias, int K, i
 }
 
 int dense_mx8(const Mx8W& w, int flags, const void* A, int64_t lda, const uint32_t* as, void* C,
-              int64_t ldc, uint32_t* cs, int M, const void* resid, int64_t ldr, hipStream_t s) {
+              int64_t ldc, uint32_t* cs, int M, const void* resid, int64_t ldr, hipStream_t s,
+              const float* rstats = nullptr, const float* rgamma = nullptr,
+              const float* rbeta = nullptr) {
   Mx8GemmParams p{};
   p.A = (const uint8_t*)A; p.lda = lda; p.As = as; p.ldas = M;
   p.W = (const uint8_t*)w.w; p.ldw = w.kpad; p.Ws = w.s; p.ldws = w.npad;
   p.C = C; p.ldc = ldc; p.Cs = cs; p.ldcs = M;
   p.M = M; p.N = w.N; p.K = w.kpad;
   p.bias = w.b; p.resid = resid; p.ldr = ldr;
+  p.rstats = rstats; p.rgamma = rgamma; p.rbeta = rbeta;
   EVT_HIP(gemm_mx8_launch(flags, p, s), "dense_mx8");
   return EVT_OK;
 }
@@ -273,12 +276,12 @@ size_t workspace_bytes(const evt_vit_desc* d, const Shape& sh, int B) {
   const size_t rows = (size_t)B * sh.T;
   const size_t hb = std::max(rows * sh.max_ffn_st, (size_t)B * sh.P * sh.pd) * es;
   size_t extra = 0;
-  if (mx8) {  // qa + sa, qh + its scales, ybuf (run_encoder_mx8)
+  if (mx8) {  // qa + sa, qh + its scales, LayerNorm row statistics (run_encoder_mx8)
     const size_t qa = std::max(round_up(sh.D, 128), round_up(sh.max_inner, 128));
     int maxffn = 0;
     for (int i = 0; i < d->depth; ++i) maxffn = std::max(maxffn, (int)d->ffn[i]);
     const size_t qh = round_up(maxffn, 128);
-    extra = rows * (qa + qa / 32 + qh + qh / 32 + 2 * sh.D) + 5 * 256;
+    extra = rows * (qa + qa / 32 + qh + qh / 32 + 2 * sizeof(float)) + 5 * 256;
   }
   return 2 * rows * sh.D * es + 2 * rows * stats_slots(sh.D) * 2 * sizeof(float) +
          rows * 3 * sh.max_inner * es +
@@ -449,14 +452,15 @@ int run_encoder(evt_model* m, int B, hipStream_t s) {
 }
 
 // MX8 encoder (reference semantics, transformer_encoder.py:13-18): per sublayer the LayerNorm
-// runs in the quantizer (y = LN(x) kept in bf16 as the residual, norm.py:11-12 + residual.py:9),
-// the Dense layers on the block-scaled MFMA, FC1's GELU output re-quantized in its epilogue.
+// runs in the quantizer (which keeps each row's (mu, rstd)), the Dense layers on the block-scaled
+// MFMA, the residual LN(x) (norm.py:11-12 + residual.py:9) re-formed in the out-proj / FC2
+// epilogues from x and those statistics, FC1's GELU output re-quantized in its epilogue.
 int run_encoder_mx8(evt_model* m, int B, hipStream_t s) {
   const int D = m->D, T = m->sh.T, rows = B * T;
   const float log2e = 1.4426950408889634f;
   const int dpad = (int)round_up(D, 128);
   for (const Layer& L : m->layers) {
-    EVT_HIP(ln_mx8_launch(m->x, rows, D, dpad, L.ln1_g, L.ln1_b, m->eps, m->ybuf, m->qa, m->sa, s),
+    EVT_HIP(ln_mx8_launch(m->x, rows, D, dpad, L.ln1_g, L.ln1_b, m->eps, m->lnst, m->qa, m->sa, s),
             "ln1 mx8");
     EVT_RC(dense_mx8(L.mqkv, EPI_BIAS, m->qa, dpad, m->sa, m->qkv, 3 * L.inner, nullptr, rows,
                      nullptr, 0, s));
@@ -466,14 +470,15 @@ int run_encoder_mx8(evt_model* m, int B, hipStream_t s) {
     EVT_HIP(mx8_quantize_launch(DT_BF16, m->o, L.inner, rows, L.inner, ipad, m->qa, ipad, m->sa,
                                 rows, s),
             "quantize attn out");
-    EVT_RC(dense_mx8(L.mout, EPI_BIAS | EPI_RESID, m->qa, ipad, m->sa, m->xm, D, nullptr, rows,
-                     m->ybuf, D, s));
-    EVT_HIP(ln_mx8_launch(m->xm, rows, D, dpad, L.ln2_g, L.ln2_b, m->eps, m->ybuf, m->qa, m->sa, s),
+    EVT_RC(dense_mx8(L.mout, EPI_BIAS | EPI_RESID | EPI_RESLN, m->qa, ipad, m->sa, m->xm, D,
+                     nullptr, rows, m->x, D, s, m->lnst, L.ln1_g, L.ln1_b));
+    EVT_HIP(ln_mx8_launch(m->xm, rows, D, dpad, L.ln2_g, L.ln2_b, m->eps, m->lnst, m->qa, m->sa,
+                          s),
             "ln2 mx8");
     EVT_RC(dense_mx8(L.mfc1, EPI_BIAS | EPI_GELU | EPI_OUT_MX8, m->qa, dpad, m->sa, m->qh,
                      m->qh_ld, m->shd, rows, nullptr, 0, s));
-    EVT_RC(dense_mx8(L.mfc2, EPI_BIAS | EPI_RESID, m->qh, m->qh_ld, m->shd, m->x, D, nullptr,
-                     rows, m->ybuf, D, s));
+    EVT_RC(dense_mx8(L.mfc2, EPI_BIAS | EPI_RESID | EPI_RESLN, m->qh, m->qh_ld, m->shd, m->x, D,
+                     nullptr, rows, m->xm, D, s, m->lnst, L.ln2_g, L.ln2_b));
   }
   return EVT_OK;
 }
@@ -727,7 +732,7 @@ int evt_vit_create(const evt_vit_desc* desc, const float* const* w, int n_weight
       EVT_RC(dev_alloc(m, (void**)&m->sa, rows * (m->qa_ld / 128) * 4));
       EVT_RC(dev_alloc(m, &m->qh, rows * m->qh_ld));
       EVT_RC(dev_alloc(m, (void**)&m->shd, rows * (m->qh_ld / 128) * 4));
-      EVT_RC(dev_alloc(m, &m->ybuf, rows * D * 2));
+      EVT_RC(dev_alloc(m, (void**)&m->lnst, rows * 2 * sizeof(float)));
       // FC1 writes columns < roundup(ffn, 32) only: the rest of the FC2 operand stays zero
       EVT_HIP(hipMemsetAsync(m->qh, 0, rows * m->qh_ld, s), "memset qh");
       EVT_HIP(hipMemsetAsync(m->shd, 0, rows * (m->qh_ld / 128) * 4, s), "memset qh scales");
@@ -1244,6 +1249,8 @@ int evt_dense_mx8(const evt_dense_mx8_args* a, void* stream) {
   if ((f & EPI_BIAS) && !a->bias) return fail(EVT_EINVAL, "dense_mx8: bias flag without bias");
   if ((f & EPI_RESID) && (!a->resid || a->ldr < a->N || a->ldr % 8))
     return fail(EVT_EINVAL, "dense_mx8: bad resid");
+  if (f & (EPI_RESLN | EPI_LNIN | EPI_STATS | EPI_POS))
+    return fail(EVT_EINVAL, "dense_mx8: unsupported flags");
   if ((f & EPI_OUT_MX8) && (!a->c_scales || a->N % 32 || a->ld_cs < a->M))
     return fail(EVT_EINVAL, "dense_mx8: MX8 output needs c_scales, N % 32, ld_cs >= M");
   Mx8GemmParams p{};

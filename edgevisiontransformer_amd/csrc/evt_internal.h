@@ -189,16 +189,19 @@ struct Mx8GemmParams {
   int M, N, K;                      // K multiple of 128, N multiple of 8
   const float* bias;                // >= N floats
   const void* resid; int64_t ldr;   // bf16
+  const float* rstats;              // EPI_RESLN: [M] (mu, rstd) of the resid rows (ln_mx8_launch)
+  const float* rgamma;              // EPI_RESLN: LayerNorm gamma / beta [N]
+  const float* rbeta;
 };
 hipError_t mx8_quantize_launch(int in_dtype, const void* x, int64_t ldx, int rows, int K, int Kpad,
                                void* q, int64_t ldq, uint32_t* s, int64_t lds, hipStream_t st);
 hipError_t mx8_pack_launch(const float* W, const float* row_scale, int K, int N, void* Wq, int Kpad,
                            int Npad, uint32_t* s, hipStream_t st);
 hipError_t gemm_mx8_launch(int flags, const Mx8GemmParams& p, hipStream_t s);
-// LayerNorm of bf16 rows [rows][D] -> y bf16 [rows][D] (if y) and MX8 q [rows][Kpad] +
-// scales [Kpad/128][rows]; D % 8 == 0, D <= Kpad <= 1024.
+// LayerNorm of bf16 rows [rows][D] -> MX8 q [rows][Kpad] + scales [Kpad/128][rows] and, if
+// stats, (mu, rstd) per row [rows][2]; D % 8 == 0, D <= Kpad <= 1024.
 hipError_t ln_mx8_launch(const void* x, int rows, int D, int Kpad, const float* gamma,
-                         const float* beta, float eps, void* y, void* q, uint32_t* s,
+                         const float* beta, float eps, float* stats, void* q, uint32_t* s,
                          hipStream_t st);
 
 }  // namespace evt

@@ -96,13 +96,15 @@ __global__ __launch_bounds__(256) void mx8_quantize_kernel(const T* __restrict__
 
 // ---- LayerNorm + MX8 quantization of a bf16 token stream (the MX8 model's LN1 / LN2) --------
 // One wave per row: y = (x - mu) * rsqrt(var + eps) * gamma + beta (population variance, Keras
-// LayerNormalization, reference norm.py:6), written as bf16 (the reference block's residual is
-// LN(x), norm.py:11-12) when y != null, and as MX8 [Kpad] (columns past D quantized as zeros).
+// LayerNormalization, reference norm.py:6) written as MX8 [Kpad] (columns past D quantized as
+// zeros), and (mu, rstd) per row when stats != null: the consumer GEMM re-forms the reference
+// block's residual LN(x) (norm.py:11-12) in its epilogue (EPI_RESLN) instead of a bf16 copy.
 // Lane l owns 8-element chunks l, l + 64 (D <= 1024); 4 consecutive chunks = one MX block.
 __global__ __launch_bounds__(256) void ln_mx8_kernel(const bf16* __restrict__ x, int rows, int D,
                                                      int Kpad, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, float eps,
-                                                     bf16* __restrict__ y, uint8_t* __restrict__ q,
+                                                     f32x2* __restrict__ stats,
+                                                     uint8_t* __restrict__ q,
                                                      uint32_t* __restrict__ s) {
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -137,6 +139,7 @@ __global__ __launch_bounds__(256) void ln_mx8_kernel(const bf16* __restrict__ x,
         sq += d * d;
       }
   const float rstd = rsqrtf(wave_sum(sq) / (float)D + eps);
+  if (stats && lane == 0) stats[r] = f32x2{mu, rstd};
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int c = lane + 64 * it;
@@ -149,13 +152,6 @@ __global__ __launch_bounds__(256) void ln_mx8_kernel(const bf16* __restrict__ x,
       const float bb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[it][e] = (v[it][e] - mu) * rstd * gg[e] + bb[e];
-      if (y) {
-        const bf16x8 o = {(bf16)v[it][0], (bf16)v[it][1], (bf16)v[it][2], (bf16)v[it][3],
-                          (bf16)v[it][4], (bf16)v[it][5], (bf16)v[it][6], (bf16)v[it][7]};
-        *(bf16x8*)(y + (int64_t)r * D + 8 * c) = o;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[it][e] = (float)o[e];  // quantize what the residual holds
-      }
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[it][e] = 0.f;
@@ -238,10 +234,16 @@ __device__ __forceinline__ void mx8_epilogue(const Mx8GemmParams& p, const f32x4
   for (int pp = 0; pp < 2; ++pp) {
     const int n = n0 + wn * 64 + pp * 32 + 8 * g;
     const bool nok = n < p.N;
-    f32x4 b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
+    f32x4 b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0, g0 = b0, g1 = b0, e0 = b0, e1 = b0;
     if ((FL & EPI_BIAS) && nok) {
       b0 = *(const f32x4*)(p.bias + n);
       b1 = *(const f32x4*)(p.bias + n + 4);
+    }
+    if ((FL & EPI_RESLN) && nok) {  // LayerNorm gamma / beta of the residual
+      g0 = *(const f32x4*)(p.rgamma + n);
+      g1 = *(const f32x4*)(p.rgamma + n + 4);
+      e0 = *(const f32x4*)(p.rbeta + n);
+      e1 = *(const f32x4*)(p.rbeta + n + 4);
     }
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
@@ -259,8 +261,15 @@ __device__ __forceinline__ void mx8_epilogue(const Mx8GemmParams& p, const f32x4
       }
       if ((FL & EPI_RESID) && ok) {
         const bf16x8 r8 = *(const bf16x8*)((const bf16*)p.resid + (int64_t)m * p.ldr + n);
-        lo += f32x4{(float)r8[0], (float)r8[1], (float)r8[2], (float)r8[3]};
-        hi += f32x4{(float)r8[4], (float)r8[5], (float)r8[6], (float)r8[7]};
+        f32x4 rlo = {(float)r8[0], (float)r8[1], (float)r8[2], (float)r8[3]};
+        f32x4 rhi = {(float)r8[4], (float)r8[5], (float)r8[6], (float)r8[7]};
+        if (FL & EPI_RESLN) {  // residual LN(resid) from the row's (mu, rstd)
+          const f32x2 st = ((const f32x2*)p.rstats)[m];
+          rlo = (rlo - st[0]) * st[1] * g0 + e0;
+          rhi = (rhi - st[0]) * st[1] * g1 + e1;
+        }
+        lo += rlo;
+        hi += rhi;
       }
       if constexpr ((FL & EPI_OUT_MX8) != 0) {
         float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -487,12 +496,12 @@ hipError_t mx8_quantize_launch(int in_dtype, const void* x, int64_t ldx, int row
 }
 
 hipError_t ln_mx8_launch(const void* x, int rows, int D, int Kpad, const float* gamma,
-                         const float* beta, float eps, void* y, void* q, uint32_t* s,
+                         const float* beta, float eps, float* stats, void* q, uint32_t* s,
                          hipStream_t st) {
   if (rows <= 0) return hipSuccess;
   if (D % 8 || D > 1024 || Kpad % 128 || Kpad < D || Kpad > 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(ln_mx8_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, (const bf16*)x, rows,
-                     D, Kpad, gamma, beta, eps, (bf16*)y, (uint8_t*)q, s);
+                     D, Kpad, gamma, beta, eps, (f32x2*)stats, (uint8_t*)q, s);
   return hipGetLastError();
 }
 
@@ -512,6 +521,8 @@ hipError_t gemm_mx8_launch(int flags, const Mx8GemmParams& p, hipStream_t s) {
     case EPI_BIAS | EPI_GELU: return launch_mx8<EPI_BIAS | EPI_GELU>(p, s);
     case EPI_BIAS | EPI_GELU_ERF: return launch_mx8<EPI_BIAS | EPI_GELU_ERF>(p, s);
     case EPI_BIAS | EPI_RESID: return launch_mx8<EPI_BIAS | EPI_RESID>(p, s);
+    case EPI_BIAS | EPI_RESID | EPI_RESLN:  // the MX8 model's out-proj / FC2 (capi.cpp)
+      return launch_mx8<EPI_BIAS | EPI_RESID | EPI_RESLN>(p, s);
     case EPI_OUT_F32: return launch_mx8<EPI_OUT_F32>(p, s);
     case EPI_BIAS | EPI_OUT_F32: return launch_mx8<EPI_BIAS | EPI_OUT_F32>(p, s);
     case EPI_BIAS | EPI_GELU | EPI_OUT_F32: return launch_mx8<EPI_BIAS | EPI_GELU | EPI_OUT_F32>(p, s);
