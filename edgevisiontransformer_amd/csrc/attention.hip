@@ -147,6 +147,42 @@ __device__ __forceinline__ void attn_tile_bf16(const AttnParams& p, const EVT_LD
   }
   // o[dt][j] = O^T[d = dt*16 + 4g + j][query]
   const int q = qt * 16 + c16;
+  if (p.q8) {  // MX8 output: 32-feature block blk = dt pair (2 blk, 2 blk + 1), 4 lanes per query
+    const float inv = 1.0f / sum;
+    const int64_t row = (int64_t)b * p.N + q;
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+      const f32x4 lo = o[2 * blk] * inv, hi = o[2 * blk + 1] * inv;
+      float am = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) am = fmaxf(am, fmaxf(fabsf(lo[j]), fabsf(hi[j])));
+      am = fmaxf(am, __shfl_xor(am, 16, 64));
+      am = fmaxf(am, __shfl_xor(am, 32, 64));
+      const int E = (int)((__float_as_uint(am) >> 23) & 0xff);
+      const unsigned sb = (unsigned)max(E - 8, 0);  // OCP MX shared exponent (mx8.hip)
+      const float is = __uint_as_float((254u - sb) << 23);
+      float c[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        c[j] = __builtin_amdgcn_fmed3f(lo[j] * is, -448.f, 448.f);
+        c[4 + j] = __builtin_amdgcn_fmed3f(hi[j] * is, -448.f, 448.f);
+      }
+      int w0 = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+      w0 = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], w0, true);
+      int w1 = __builtin_amdgcn_cvt_pk_fp8_f32(c[4], c[5], 0, false);
+      w1 = __builtin_amdgcn_cvt_pk_fp8_f32(c[6], c[7], w1, true);
+      if (q < p.N) {
+        uint8_t* dst = p.q8 + row * p.ldq8 + h * 64 + 32 * blk + 4 * g;
+        *(int*)dst = w0;
+        *(int*)(dst + 16) = w1;
+        if (g == 0) {
+          const int bi = 2 * h + blk;
+          ((uint8_t*)p.s8)[((int64_t)(bi >> 2) * p.rows8 + row) * 4 + (bi & 3)] = (uint8_t)sb;
+        }
+      }
+    }
+    return;
+  }
   if (q < p.N) {
     const float inv = 1.0f / sum;
     bf16* op = (bf16*)p.out + ((int64_t)b * p.N + q) * p.ldo + h * 64 + 4 * g;

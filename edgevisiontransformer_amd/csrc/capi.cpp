@@ -454,7 +454,8 @@ int run_encoder(evt_model* m, int B, hipStream_t s) {
 // MX8 encoder (reference semantics, transformer_encoder.py:13-18): per sublayer the LayerNorm
 // runs in the quantizer (which keeps each row's (mu, rstd)), the Dense layers on the block-scaled
 // MFMA, the residual LN(x) (norm.py:11-12 + residual.py:9) re-formed in the out-proj / FC2
-// epilogues from x and those statistics, FC1's GELU output re-quantized in its epilogue.
+// epilogues from x and those statistics; the attention and FC1 (GELU) outputs are quantized in
+// their producing kernels' epilogues.
 int run_encoder_mx8(evt_model* m, int B, hipStream_t s) {
   const int D = m->D, T = m->sh.T, rows = B * T;
   const float log2e = 1.4426950408889634f;
@@ -464,12 +465,15 @@ int run_encoder_mx8(evt_model* m, int B, hipStream_t s) {
             "ln1 mx8");
     EVT_RC(dense_mx8(L.mqkv, EPI_BIAS, m->qa, dpad, m->sa, m->qkv, 3 * L.inner, nullptr, rows,
                      nullptr, 0, s));
-    AttnParams ap{m->qkv, 3 * L.inner, m->o, L.inner, T, L.heads, B, 0.125f * log2e};
-    EVT_HIP(attention_launch(DT_BF16, ap, s), "attention");
+    // attention writes O straight as the MX8 operand of the out-proj (columns [inner, ipad) of
+    // qa keep finite stale values, cancelled by the zero rows of the packed weights)
     const int ipad = L.mout.kpad;
-    EVT_HIP(mx8_quantize_launch(DT_BF16, m->o, L.inner, rows, L.inner, ipad, m->qa, ipad, m->sa,
-                                rows, s),
-            "quantize attn out");
+    AttnParams ap{m->qkv, 3 * L.inner, m->o, L.inner, T, L.heads, B, 0.125f * log2e};
+    ap.q8 = (uint8_t*)m->qa;
+    ap.s8 = m->sa;
+    ap.ldq8 = ipad;
+    ap.rows8 = rows;
+    EVT_HIP(attention_launch(DT_BF16, ap, s), "attention");
     EVT_RC(dense_mx8(L.mout, EPI_BIAS | EPI_RESID | EPI_RESLN, m->qa, ipad, m->sa, m->xm, D,
                      nullptr, rows, m->x, D, s, m->lnst, L.ln1_g, L.ln1_b));
     EVT_HIP(ln_mx8_launch(m->xm, rows, D, dpad, L.ln2_g, L.ln2_b, m->eps, m->lnst, m->qa, m->sa,
@@ -733,6 +737,9 @@ int evt_vit_create(const evt_vit_desc* desc, const float* const* w, int n_weight
       EVT_RC(dev_alloc(m, &m->qh, rows * m->qh_ld));
       EVT_RC(dev_alloc(m, (void**)&m->shd, rows * (m->qh_ld / 128) * 4));
       EVT_RC(dev_alloc(m, (void**)&m->lnst, rows * 2 * sizeof(float)));
+      // every byte of the MX8 operands is written finite before it is read (NaN-free padding)
+      EVT_HIP(hipMemsetAsync(m->qa, 0, rows * m->qa_ld, s), "memset qa");
+      EVT_HIP(hipMemsetAsync(m->sa, 0, rows * (m->qa_ld / 128) * 4, s), "memset qa scales");
       // FC1 writes columns < roundup(ffn, 32) only: the rest of the FC2 operand stays zero
       EVT_HIP(hipMemsetAsync(m->qh, 0, rows * m->qh_ld, s), "memset qh");
       EVT_HIP(hipMemsetAsync(m->shd, 0, rows * (m->qh_ld / 128) * 4, s), "memset qh scales");

@@ -75,6 +75,12 @@ struct AttnParams {
   int H;                          // heads; head_dim is fixed at 64
   int B;                          // images
   float scale_log2;               // head_dim^-0.5 * log2(e)
+  // bf16 only: when q8 is set, O is written as MX8 instead (e4m3 bytes q8[row][ldq8], scales
+  // s8[ldq8/128][rows8] dwords; the MX8 model's out-proj operand) and `out` is not written
+  uint8_t* q8 = nullptr;
+  uint32_t* s8 = nullptr;
+  int64_t ldq8 = 0;
+  int rows8 = 0;
 };
 hipError_t attention_launch(int dtype, const AttnParams& p, hipStream_t s);
 
