@@ -167,12 +167,13 @@ __global__ __launch_bounds__(256) void ln_mx8_kernel(const bf16* __restrict__ x,
 #pragma unroll
     for (int e = 0; e < 8; ++e) t[e] = v[it][e] * inv;
     const u32x2 o8 = mx8_pack8(t);
+    // the 4 scale bytes of a 128-column k-step come from lanes c, c+4, c+8, c+12 (c % 16 == 0):
+    // gather them into one dword store instead of 4 byte stores
+    const unsigned s1 = __shfl_down(sb, 4, 64), s2 = __shfl_down(sb, 8, 64),
+                   s3 = __shfl_down(sb, 12, 64);
     if (c < nq) {
       *(u32x2*)(q + (int64_t)r * Kpad + 8 * c) = o8;
-      if ((c & 3) == 0) {
-        const int blk = c >> 2;
-        ((uint8_t*)s)[((int64_t)(blk >> 2) * rows + r) * 4 + (blk & 3)] = (uint8_t)sb;
-      }
+      if ((c & 15) == 0) s[(int64_t)(c >> 4) * rows + r] = sb | (s1 << 8) | (s2 << 16) | (s3 << 24);
     }
   }
 }
