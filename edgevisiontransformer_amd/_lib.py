@@ -70,7 +70,9 @@ class evt_dense_mx8_args(ctypes.Structure):
                 ("w_scales", ctypes.c_void_p), ("C", ctypes.c_void_p), ("ldc", ctypes.c_int64),
                 ("c_scales", ctypes.c_void_p), ("ld_cs", ctypes.c_int64),
                 ("M", ctypes.c_int32), ("N", ctypes.c_int32), ("bias", ctypes.c_void_p),
-                ("resid", ctypes.c_void_p), ("ldr", ctypes.c_int64)]
+                ("resid", ctypes.c_void_p), ("ldr", ctypes.c_int64),
+                ("rstats", ctypes.c_void_p), ("rgamma", ctypes.c_void_p),
+                ("rbeta", ctypes.c_void_p)]
 
 
 class evt_t2t_desc(ctypes.Structure):
@@ -132,6 +134,8 @@ SIGNATURES = {
     "evt_mx8_quantize": (_I, [_I, _P, _I64, _I, _I, _I, _P, _I64, _P, _I64, _P]),
     "evt_mx8_pack_weight": (_I, [_P, _P, _I, _I, _P, _I, _I, _P, _P]),
     "evt_dense_mx8": (_I, [ctypes.POINTER(evt_dense_mx8_args), _P]),
+    "evt_mx8_layernorm": (_I, [_P, _I, _I, _I, _P, _P, _F, _P, _P, _P, _P]),
+    "evt_attention_mx8": (_I, [_P, _I64, _P, _I64, _P, _I64, _I, _I, _I, _F, _P]),
 }
 
 _lib = None

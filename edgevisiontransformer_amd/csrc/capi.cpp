@@ -1256,7 +1256,9 @@ int evt_dense_mx8(const evt_dense_mx8_args* a, void* stream) {
   if ((f & EPI_BIAS) && !a->bias) return fail(EVT_EINVAL, "dense_mx8: bias flag without bias");
   if ((f & EPI_RESID) && (!a->resid || a->ldr < a->N || a->ldr % 8))
     return fail(EVT_EINVAL, "dense_mx8: bad resid");
-  if (f & (EPI_RESLN | EPI_LNIN | EPI_STATS | EPI_POS))
+  if ((f & EPI_RESLN) && (!(f & EPI_RESID) || !a->rstats || !a->rgamma || !a->rbeta))
+    return fail(EVT_EINVAL, "dense_mx8: LN residual needs resid, rstats, rgamma, rbeta");
+  if (f & (EPI_LNIN | EPI_STATS | EPI_POS))
     return fail(EVT_EINVAL, "dense_mx8: unsupported flags");
   if ((f & EPI_OUT_MX8) && (!a->c_scales || a->N % 32 || a->ld_cs < a->M))
     return fail(EVT_EINVAL, "dense_mx8: MX8 output needs c_scales, N % 32, ld_cs >= M");
@@ -1266,9 +1268,39 @@ int evt_dense_mx8(const evt_dense_mx8_args* a, void* stream) {
   p.C = a->C; p.ldc = a->ldc; p.Cs = a->c_scales; p.ldcs = a->ld_cs;
   p.M = a->M; p.N = a->N; p.K = a->Kpad;
   p.bias = a->bias; p.resid = a->resid; p.ldr = a->ldr;
+  p.rstats = a->rstats; p.rgamma = a->rgamma; p.rbeta = a->rbeta;
   hipError_t e = gemm_mx8_launch(f, p, (hipStream_t)stream);
   if (e == hipErrorInvalidValue) return fail(EVT_EINVAL, "dense_mx8: unsupported flags");
   EVT_HIP(e, "dense_mx8");
+  return EVT_OK;
+}
+
+int evt_mx8_layernorm(const void* x, int rows, int D, int Kpad, const float* gamma,
+                      const float* beta, float eps, float* stats, void* q, uint32_t* scales,
+                      void* stream) {
+  if (!x || !gamma || !beta || !q || !scales || rows < 0 || D <= 0 || D % 8 || D > Kpad ||
+      Kpad % 128 || Kpad > 1024 || !(eps > 0.f))
+    return fail(EVT_EINVAL, "mx8_layernorm: bad shape (D % 8, D <= Kpad <= 1024, Kpad % 128)");
+  if ((((uintptr_t)x | (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)q) & 15) ||
+      (((uintptr_t)scales | (uintptr_t)stats) & 7))
+    return fail(EVT_EINVAL, "mx8_layernorm: misaligned pointer");
+  EVT_HIP(ln_mx8_launch(x, rows, D, Kpad, gamma, beta, eps, stats, q, scales,
+                        (hipStream_t)stream),
+          "mx8_layernorm");
+  return EVT_OK;
+}
+
+int evt_attention_mx8(const void* qkv, int64_t ldq, void* q8, int64_t ldq8, uint32_t* s8,
+                      int64_t ld_s8, int B, int N, int H, float scale, void* stream) {
+  if (!qkv || !q8 || !s8 || B < 0 || N <= 0 || N > 256 || H <= 0 || ldq < 3 * H * 64 ||
+      ldq % 8 || ldq8 < H * 64 || ldq8 % 128 || ld_s8 < (int64_t)B * N || ld_s8 > INT32_MAX)
+    return fail(EVT_EINVAL, "attention_mx8: bad shape (N <= 256, head size 64, ldq8 % 128)");
+  AttnParams p{qkv, ldq, nullptr, 0, N, H, B, scale * 1.4426950408889634f};
+  p.q8 = (uint8_t*)q8;
+  p.s8 = s8;
+  p.ldq8 = ldq8;
+  p.rows8 = (int)ld_s8;
+  EVT_HIP(attention_launch(DT_BF16, p, (hipStream_t)stream), "attention_mx8");
   return EVT_OK;
 }
 

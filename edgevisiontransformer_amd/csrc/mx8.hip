@@ -21,6 +21,8 @@
 // (D^T = W . X^T) with the W rows of each 32-column pair interleaved, so every lane ends with 8
 // consecutive output columns of one row: 16-B bf16 stores, and a 32-column MX block of the output
 // spans exactly the 4 lane groups of one row (2 shuffles for its amax).
+#include <mutex>
+
 #include "common.h"
 #include "evt_internal.h"
 
@@ -459,20 +461,33 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(Mx8GemmParams p) {
   }
 }
 
+// Per-device launch state: the dynamic-LDS attribute of each kernel instantiation (set once per
+// device, return code checked) and the device's CU count. Guarded by a mutex: the first calls
+// from two threads, or on two devices, must not race on the caches.
+constexpr int MX_MAX_DEV = 64;
+std::mutex g_mx8_mu;
+int g_mx8_cus[MX_MAX_DEV];
+
 template <int FL>
 hipError_t launch_mx8(const Mx8GemmParams& p, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    attr = true;
-    (void)hipFuncSetAttribute((const void*)gemm_mx8_kernel<FL>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, MX_NSTAGE * MX_STAGE);
-  }
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
+  static bool attr[MX_MAX_DEV];
+  int dev = 0, cus = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= MX_MAX_DEV) return hipErrorInvalidDevice;
+  {
+    std::lock_guard<std::mutex> lk(g_mx8_mu);
+    if (!attr[dev]) {
+      e = hipFuncSetAttribute((const void*)gemm_mx8_kernel<FL>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, MX_NSTAGE * MX_STAGE);
+      if (e != hipSuccess) return e;
+      attr[dev] = true;
+    }
+    if (!g_mx8_cus[dev]) {
+      e = hipDeviceGetAttribute(&g_mx8_cus[dev], hipDeviceAttributeMultiprocessorCount, dev);
+      if (e != hipSuccess || g_mx8_cus[dev] <= 0) g_mx8_cus[dev] = 256;
+    }
+    cus = g_mx8_cus[dev];
   }
   const int nb = ((p.M + MX_BM - 1) / MX_BM) * ((p.N + MX_BN - 1) / MX_BN);
   const int grid = min(nb, cus);  // one resident 8-wave workgroup per CU (148.5 KiB of LDS)

@@ -35,6 +35,17 @@ def _ptr(t: Optional[torch.Tensor]):
     return ctypes.c_void_p(t.data_ptr() if t is not None else 0)
 
 
+def _aligned_rows(t: torch.Tensor) -> torch.Tensor:
+    """The kernels read rows with 16-B vector loads: rows must be contiguous, 16-B aligned and a
+    multiple of 16 B apart. A view that is not (e.g. a column slice) is copied."""
+    esz = t.element_size()
+    if t.stride(-1) != 1 or t.data_ptr() % 16 or (t.dim() == 2 and (t.stride(0) * esz) % 16):
+        t = t.contiguous()
+        if t.data_ptr() % 16 or (t.dim() == 2 and (t.stride(0) * esz) % 16):
+            raise ValueError("MX8: rows must be 16-B aligned (row width a multiple of 16 bytes)")
+    return t
+
+
 class MX8Tensor:
     """An MX8 matrix on the device: e4m3 bytes q [rows, Kpad] and scale dwords [Kpad/128, rows]."""
 
@@ -51,8 +62,9 @@ def quantize_mx8(x: torch.Tensor) -> MX8Tensor:
     if x.dim() != 2 or not x.is_cuda or x.dtype not in (torch.bfloat16, torch.float32):
         raise ValueError("quantize_mx8: expects a 2-D bf16 / fp32 device tensor")
     rows, K = x.shape
-    if K % 8 or x.stride(1) != 1:
-        raise ValueError("quantize_mx8: K must be a multiple of 8, rows contiguous")
+    if K % 8:
+        raise ValueError("quantize_mx8: K must be a multiple of 8")
+    x = _aligned_rows(x)
     _lib.ensure_device(x.device.index or 0)
     kpad = _round_up(K, 128)
     q = torch.empty((rows, kpad), dtype=torch.uint8, device=x.device)
@@ -108,6 +120,7 @@ class MX8Dense:
                 raise ValueError("MX8Dense: residual must be [rows, units] bf16")
             if flags & (_lib.EPI_GELU | _lib.EPI_GELU_ERF) or out_dtype != torch.bfloat16:
                 raise ValueError("MX8Dense: residual fuses with a linear bf16-output layer only")
+            residual = _aligned_rows(residual)
             flags |= _lib.EPI_RESID
         if out_dtype == torch.float32:
             flags |= _lib.EPI_OUT_F32

@@ -344,12 +344,30 @@ typedef struct evt_dense_mx8_args {
   int32_t M, N;                      /* N % 8 == 0 */
   const float* bias;
   const void* resid; int64_t ldr;    /* bf16 */
+  const float* rstats;               /* EVT_EPI_RESLN: [M][2] (mu, rstd) of the resid rows, as
+                                        evt_mx8_layernorm writes them */
+  const float* rgamma; const float* rbeta; /* EVT_EPI_RESLN: LayerNorm gamma / beta [N] */
 } evt_dense_mx8_args;
 
 /* Dense layer on MX8 operands (tf.keras.layers.Dense on the quantized model):
  * C = epi(dequant(A) . dequant(W)), fp32 accumulation; flag sets 0, 1, 3, 257, 5, 16, 17, 19,
- * 273, 512, 513, 515, 769. */
+ * 273, 512, 513, 515, 769, and 69 (bias + residual LN(resid) re-formed from rstats: the MX8
+ * model's out-proj / FC2, reference norm.py:11-12 + residual.py:9). */
 int evt_dense_mx8(const evt_dense_mx8_args* args, void* stream);
+
+/* LayerNormalization(epsilon) of bf16 rows x [rows][D] (reference norm.py:6, population variance)
+ * quantized straight to MX8: q [rows][Kpad] e4m3 (columns [D, Kpad) quantized as zeros), scales
+ * [Kpad/128][rows] dwords, and, if stats != NULL, (mu, rstd) per row [rows][2] for a consumer's
+ * EVT_EPI_RESLN. D % 8 == 0, D <= Kpad <= 1024, Kpad % 128 == 0. The MX8 model's LN1 / LN2. */
+int evt_mx8_layernorm(const void* x, int rows, int D, int Kpad, const float* gamma,
+                      const float* beta, float eps, float* stats, void* q, uint32_t* scales,
+                      void* stream);
+
+/* evt_attention (bf16 qkv, head size 64) with the output O written as MX8 instead of bf16:
+ * q8 [B*N][ldq8] e4m3 (columns (h d)), scales s8[ldq8/128][ld_s8] dwords (ld_s8 >= B*N): the
+ * MX8 model's out-proj operand (attention.py:20-35). ldq8 % 128 == 0, ldq8 >= 64*H. */
+int evt_attention_mx8(const void* qkv, int64_t ldq, void* q8, int64_t ldq8, uint32_t* s8,
+                      int64_t ld_s8, int B, int N, int H, float scale, void* stream);
 
 #ifdef __cplusplus
 }

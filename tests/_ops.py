@@ -116,7 +116,31 @@ def mx8_pack(W: torch.Tensor, row_scale: torch.Tensor = None):
     return wq, s, kpad, npad
 
 
-def dense_mx8(flags, Aq, As, wq, ws, kpad, npad, M, N, bias=None, resid=None):
+def mx8_layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, Kpad: int,
+                  eps: float = 1e-5):
+    """bf16 rows [rows, D] -> (q uint8 [rows, Kpad], scale dwords [Kpad/128, rows],
+    (mu, rstd) fp32 [rows, 2]) through evt_mx8_layernorm."""
+    rows, D = x.shape
+    q = torch.full((rows, Kpad), 0x7F, dtype=torch.uint8, device=x.device)  # NaN fill: all written
+    s = torch.full((Kpad // 128, rows), 0x7F7F7F7F, dtype=torch.int32, device=x.device)
+    st = torch.full((rows, 2), float("nan"), dtype=torch.float32, device=x.device)
+    _lib.check(_lib.load_library().evt_mx8_layernorm(_p(x), rows, D, Kpad, _p(gamma), _p(beta), eps,
+                                                     _p(st), _p(q), _p(s), _s()))
+    return q, s, st
+
+
+def attention_mx8(qkv: torch.Tensor, B: int, N: int, H: int, scale: float = 0.125):
+    """bf16 qkv [B*N, 3*H*64] -> MX8 O (q uint8 [B*N, ldq8], scale dwords [ldq8/128, B*N])."""
+    ldq8 = round_up(H * 64, 128)
+    q = torch.full((B * N, ldq8), 0x7F, dtype=torch.uint8, device=qkv.device)
+    s = torch.full((ldq8 // 128, B * N), 0x7F7F7F7F, dtype=torch.int32, device=qkv.device)
+    _lib.check(_lib.load_library().evt_attention_mx8(_p(qkv), qkv.stride(0), _p(q), ldq8, _p(s),
+                                                     B * N, B, N, H, scale, _s()))
+    return q, s
+
+
+def dense_mx8(flags, Aq, As, wq, ws, kpad, npad, M, N, bias=None, resid=None, rstats=None,
+              rgamma=None, rbeta=None):
     a = _lib.evt_dense_mx8_args()
     a.flags, a.A, a.lda, a.a_scales, a.ld_as = flags, Aq.data_ptr(), Aq.stride(0), As.data_ptr(), As.shape[1]
     a.Wq, a.Kpad, a.Npad, a.w_scales = wq.data_ptr(), kpad, npad, ws.data_ptr()
@@ -134,5 +158,7 @@ def dense_mx8(flags, Aq, As, wq, ws, kpad, npad, M, N, bias=None, resid=None):
     a.bias = bias.data_ptr() if bias is not None else None
     a.resid = resid.data_ptr() if resid is not None else None
     a.ldr = resid.stride(0) if resid is not None else 0
+    a.rstats, a.rgamma, a.rbeta = (t.data_ptr() if t is not None else None
+                                   for t in (rstats, rgamma, rbeta))
     _lib.check(_lib.load_library().evt_dense_mx8(ctypes.byref(a), _s()))
     return (C, Cs) if Cs is not None else C

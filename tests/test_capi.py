@@ -27,7 +27,7 @@ def lib():
 def test_header_and_binding_agree():
     from edgevisiontransformer_amd import _lib
     assert _declared() == sorted(_lib.SIGNATURES)
-    assert len(_declared()) == 32
+    assert len(_declared()) == 34
 
 
 def test_every_declared_symbol_is_exported(lib):
@@ -64,6 +64,14 @@ def test_op_entry_points_validate_before_launch(lib):
     assert lib.evt_layernorm(1, None, 0, None, 0, None, None, 1, 7, 1e-5, None) == _lib.EVT_EINVAL
     assert lib.evt_pack_weight(1, None, None, 1, 1, None, 64, 128, None) == _lib.EVT_EINVAL
     assert lib.evt_dense(1, None, None) == _lib.EVT_EINVAL
+    # MX8 kernel-level entry points: shape checks before any launch
+    assert lib.evt_mx8_layernorm(None, 4, 100, 128, None, None, 1e-5, None, None, None,
+                                 None) == _lib.EVT_EINVAL
+    assert lib.evt_attention_mx8(None, 2304, None, 768, None, 394, 2, 197, 12, 0.125,
+                                 None) == _lib.EVT_EINVAL
+    a = _lib.evt_dense_mx8_args()
+    a.flags = _lib.EPI_BIAS | _lib.EPI_RESID | _lib.EPI_RESLN  # RESLN without rstats / gamma
+    assert lib.evt_dense_mx8(ctypes.byref(a), None) == _lib.EVT_EINVAL
 
 
 def test_t2t_host_validation(lib):

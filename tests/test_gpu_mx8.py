@@ -130,3 +130,139 @@ def test_dense_mx8_rejects(gpu):
         _ops.dense_mx8(2, *dev, 64, 128)  # GELU without bias: not an instantiated flag set
     with pytest.raises(RuntimeError):
         _ops.dense_mx8(0, *dev, 64, 124)  # N % 8
+
+
+# ---- kernel-level checks of the MX8 model's fused kernels (LayerNorm quantizer, LN-residual
+# epilogue, attention MX8 output). Quantization is a step function, so the device's fp32 values
+# and the fp64 restatement can land on different sides of a rounding midpoint (or of a power of
+# two for a block's scale); such elements / blocks are identified from the fp64 value and excluded
+# from the bit-exact comparison (their fraction is bounded), every other byte must match.
+def _near_midpoint(v, dv):
+    """v (already divided by the block scale) within +-dv of an e4m3 rounding midpoint."""
+    lo = mx8_ref.e4m3_round(np.clip(v - dv, -448, 448).astype(np.float32))
+    hi = mx8_ref.e4m3_round(np.clip(v + dv, -448, 448).astype(np.float32))
+    return lo != hi
+
+
+def _check_mx8_against(q, sb, y, dy, max_amb=2e-3):
+    """q bytes [R, K] / scale bytes [R, K/32] from the device vs the fp64 values y [R, K], whose
+    device-side (fp32 / bf16) counterparts differ from y by at most dy (array or scalar)."""
+    R, K = y.shape
+    dy = np.broadcast_to(np.asarray(dy, np.float64), y.shape)
+    blocks = np.abs(y).reshape(R, K // 32, 32).max(-1)
+    dblk = dy.reshape(R, K // 32, 32).max(-1)
+    sb_ref = mx8_ref.scale_bytes(blocks.astype(np.float32))
+    amb_blk = (mx8_ref.scale_bytes(np.maximum(blocks - dblk, 0).astype(np.float32)) !=
+               mx8_ref.scale_bytes((blocks + dblk).astype(np.float32)))
+    assert np.array_equal(sb[~amb_blk], sb_ref[~amb_blk])
+    inv = np.exp2(127.0 - sb_ref.astype(np.float64))
+    v = (y.reshape(R, K // 32, 32) * inv[..., None]).reshape(R, K)
+    dv = (dy.reshape(R, K // 32, 32) * inv[..., None]).reshape(R, K)
+    qr = mx8_ref.e4m3_encode(mx8_ref.e4m3_round(np.clip(v, -448, 448).astype(np.float32)))
+    amb = _near_midpoint(v, dv) | np.repeat(amb_blk, 32, axis=1)
+    dg, dr = mx8_ref.e4m3_decode(q), mx8_ref.e4m3_decode(qr)
+    assert np.array_equal(dg[~amb], dr[~amb])
+    assert amb.mean() <= max_amb, amb.mean()
+    # every element (ambiguous ones included) within one e4m3 step of its block
+    err = np.abs(mx8_ref.dequantize(q, sb) - y).reshape(R, K // 32, 32).max(-1)
+    assert np.all(err <= blocks * 2.0 ** -3 + 1e-30)
+
+
+@pytest.mark.parametrize("rows,D,Kpad", [(2 * 197 + 3, 192, 256), (301, 320, 384), (999, 768, 768),
+                                         (1003, 1024, 1024), (5, 64, 128)])
+def test_mx8_layernorm_kernel(gpu, rows, D, Kpad):
+    g = np.random.default_rng(rows + D)
+    x = (g.standard_normal((rows, D)) * np.exp2(g.integers(-3, 4, (rows, 1)))
+         + g.standard_normal((rows, 1))).astype(np.float32)
+    x[1, :] = 7.0  # constant row: variance 0 -> rstd = 1/sqrt(eps), LN(x) = beta
+    xt = torch.from_numpy(x).to(gpu).to(torch.bfloat16)
+    gamma = (1.0 + 0.2 * g.standard_normal(D)).astype(np.float32)
+    beta = (0.1 * g.standard_normal(D)).astype(np.float32)
+    q, s, st = _ops.mx8_layernorm(xt, torch.from_numpy(gamma).to(gpu),
+                                  torch.from_numpy(beta).to(gpu), Kpad)
+    torch.cuda.synchronize()
+    xb = xt.float().cpu().numpy().astype(np.float64)
+    mu = xb.mean(1)
+    rstd = 1.0 / np.sqrt(((xb - mu[:, None]) ** 2).mean(1) + 1e-5)
+    stg = st.cpu().numpy().astype(np.float64)
+    assert np.all(np.abs(stg[:, 0] - mu) <= 1e-6 * (np.abs(mu) + 1.0 / rstd))
+    assert np.all(np.abs(stg[:, 1] / rstd - 1.0) <= 1e-5)
+    y = np.zeros((rows, Kpad))
+    t = (xb - mu[:, None]) * rstd[:, None] * gamma
+    y[:, :D] = t + beta
+    # fp32 evaluation error of the device's (x - mu) * rstd * gamma + beta (incl. mu's rounding)
+    dy = np.zeros((rows, Kpad))
+    mu_err = np.where(xb.std(1) > 0, 5e-7 * np.abs(mu), 0.0)  # a constant row's mean is exact
+    dy[:, :D] = 2e-6 * (np.abs(t) + np.abs(beta)) + (mu_err * rstd)[:, None] * np.abs(gamma)
+    sb = mx8_ref.dwords_to_scales(s.cpu().numpy().view(np.uint32), rows)
+    qg = q.cpu().numpy()
+    assert np.all(qg[:, D:] & 0x7F == 0) and np.all(sb[:, (D + 31) // 32:] == 0)  # padding = zeros
+    _check_mx8_against(qg, sb, y, dy, max_amb=0.01)
+
+
+def test_mx8_layernorm_rejects(gpu):
+    x = torch.zeros((4, 100), dtype=torch.bfloat16, device=gpu)
+    gb = torch.ones(128, device=gpu)
+    with pytest.raises(RuntimeError):
+        _ops.mx8_layernorm(x, gb, gb, 128)  # D % 8
+    with pytest.raises(RuntimeError):
+        _ops.mx8_layernorm(torch.zeros((4, 256), dtype=torch.bfloat16, device=gpu), gb, gb, 128)
+
+
+@pytest.mark.parametrize("M,K,N", [(197, 768, 768), (1003, 3072, 768), (77, 384, 192)])
+def test_dense_mx8_resln(gpu, M, K, N):
+    """Flag set 69 (bias + residual LN(resid) from (mu, rstd)): the MX8 out-proj / FC2 epilogue."""
+    dev, host, mag = _operands(gpu, M, K, N, seed=3 * M + K + N)
+    g = np.random.default_rng(M)
+    bias = (0.1 * g.standard_normal(N)).astype(np.float32)
+    resid = (g.standard_normal((M, N)) * 2.0 + 0.5).astype(np.float32)
+    rt = torch.from_numpy(resid).to(gpu).to(torch.bfloat16)
+    rb = rt.float().cpu().numpy().astype(np.float64)
+    mu = rb.mean(1)
+    rstd = 1.0 / np.sqrt(((rb - mu[:, None]) ** 2).mean(1) + 1e-5)
+    rst = torch.from_numpy(np.stack([mu, rstd], 1).astype(np.float32)).to(gpu)
+    gam = (1.0 + 0.2 * g.standard_normal(N)).astype(np.float32)
+    bet = (0.1 * g.standard_normal(N)).astype(np.float32)
+    out = _ops.dense_mx8(69, *dev, M, N, bias=torch.from_numpy(bias).to(gpu), resid=rt,
+                         rstats=rst, rgamma=torch.from_numpy(gam).to(gpu),
+                         rbeta=torch.from_numpy(bet).to(gpu))
+    torch.cuda.synchronize()
+    mu32, r32 = rst.cpu().numpy()[:, 0].astype(np.float64), rst.cpu().numpy()[:, 1].astype(np.float64)
+    lnr = (rb - mu32[:, None]) * r32[:, None] * gam + bet
+    ref = mx8_ref.dense_mx8(*host, N, 1, bias=bias) + lnr
+    got = out.float().cpu().numpy()
+    tol = 3e-5 * mag + 2.0 ** -8 * np.abs(ref) + 1e-4 + 1e-5 * np.abs(lnr)
+    assert np.all(np.abs(got - ref) <= tol)
+    with pytest.raises(RuntimeError):  # RESLN without its statistics
+        _ops.dense_mx8(69, *dev, M, N, bias=torch.from_numpy(bias).to(gpu), resid=rt)
+
+
+def _attn64(qkv, B, N, H, scale=0.125):
+    q, k, v = (qkv.reshape(B, N, 3, H, 64)[:, :, i].transpose(0, 2, 1, 3) for i in range(3))
+    s = np.einsum("bhid,bhjd->bhij", q, k) * scale
+    p = np.exp(s - s.max(-1, keepdims=True))
+    p /= p.sum(-1, keepdims=True)
+    return np.einsum("bhij,bhjd->bhid", p, v).transpose(0, 2, 1, 3).reshape(B * N, H * 64)
+
+
+@pytest.mark.parametrize("B,N,H", [(2, 197, 12), (3, 197, 3), (1, 50, 6), (2, 129, 2)])
+def test_attention_mx8_kernel(gpu, B, N, H):
+    g = np.random.default_rng(B * N + H)
+    qkv = torch.from_numpy((1.5 * g.standard_normal((B * N, 3 * H * 64))).astype(np.float32))
+    qkv = qkv.to(gpu).to(torch.bfloat16)
+    q, s = _ops.attention_mx8(qkv, B, N, H)
+    o16 = _ops.attention("bf16", qkv, B, N, H)  # same kernel, bf16 output
+    torch.cuda.synchronize()
+    K = q.shape[1]
+    sb = mx8_ref.dwords_to_scales(s.cpu().numpy().view(np.uint32), B * N)[:, :H * 2]
+    qg = q.cpu().numpy()[:, :H * 64]
+    # layout / scale placement: the MX8 output equals the quantization of the same kernel's bf16
+    # output up to that output's own rounding (bf16: <= 2^-9 relative)
+    y16 = o16.float().cpu().numpy().astype(np.float64)
+    _check_mx8_against(qg, sb, y16, 1.01 * 2.0 ** -9 * np.abs(y16), max_amb=0.1)
+    # and both against the fp64 restatement (bf16 P in the PV product: 2e-2 as test_attention)
+    ref = _attn64(qkv.float().cpu().numpy().astype(np.float64), B, N, H)
+    blocks = np.abs(ref).reshape(B * N, H * 2, 32).max(-1)
+    err = np.abs(mx8_ref.dequantize(qg, sb) - ref).reshape(B * N, H * 2, 32).max(-1)
+    assert np.all(err <= blocks * 2.0 ** -3 + 2e-2)
+    assert K % 128 == 0

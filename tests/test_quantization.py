@@ -63,3 +63,16 @@ def test_mx8_feedforward_accuracy(gpu):
     cos = (got * ref).sum(1) / np.linalg.norm(got, axis=1) / np.linalg.norm(ref, axis=1)
     assert cos.min() >= 0.999, cos.min()
     assert np.abs(got - ref).max() <= 0.05 * np.abs(ref).max()
+
+
+@pytest.mark.gpu
+def test_quantize_mx8_unaligned_views(gpu):
+    """Column-sliced / odd-offset views are copied to 16-B aligned rows before the kernel's 16-B
+    loads: same bytes as the contiguous tensor."""
+    g = np.random.default_rng(2)
+    base = torch.from_numpy(g.standard_normal((64, 264)).astype(np.float32)).to(gpu).to(torch.bfloat16)
+    view = base[:, 4:260]                      # 8-B offset, stride 264 * 2 B (not 16-B aligned rows)
+    a = q.quantize_mx8(view)
+    b = q.quantize_mx8(view.contiguous())
+    torch.cuda.synchronize()
+    assert torch.equal(a.q, b.q) and torch.equal(a.scales, b.scales)
