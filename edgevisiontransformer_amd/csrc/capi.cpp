@@ -1209,8 +1209,8 @@ int evt_patch_merge(int dtype, const void* x, int64_t ldx, int B, int R, int C, 
 
 int evt_set_gemm_variant(int variant) {
   if (variant != 0 && variant != 1 && variant != 2 && variant != 6 && variant != 8 &&
-      !(variant >= 9 && variant <= 16) && variant != 106 && variant != 108)
-    return fail(EVT_EINVAL, "variant must be 0, 1, 2, 6, 8, 9-16, 106 or 108");
+      !(variant >= 9 && variant <= 19) && variant != 106 && variant != 108)
+    return fail(EVT_EINVAL, "variant must be 0, 1, 2, 6, 8, 9-19, 106 or 108");
   gemm_set_variant(variant);
   return EVT_OK;
 }

@@ -837,6 +837,8 @@ struct PersFlags {
   static constexpr bool v1 = (FL & (EPI_LNIN | EPI_RESLN)) != 0;
   static constexpr bool v2 = (FL & EPI_RESLN) != 0;
   static_assert(!((FL & EPI_LNIN) && (FL & EPI_RESLN)), "one LayerNorm source per GEMM");
+  static_assert(!(FL & EPI_RESLN) || ((FL & EPI_BIAS) && (FL & EPI_RESID)),
+                "RESLN: the residual LayerNorm's beta is folded into the bias add");
   static_assert(!(FL & (EPI_POS | EPI_OUT_F32)), "persistent kernel: bf16 outputs, no EPI_POS");
 };
 
@@ -911,10 +913,19 @@ __device__ __forceinline__ void swap_rows16(f32x4& a, f32x4& b) {
 // entirely past N skip their epilogue VALU work. Compiled out otherwise (the check alone cost
 // 2-4 % on the DeiT shapes, measured in one process).
 template <int FL, int DBG = 0, bool PADN = true>
-__device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
+__device__ __forceinline__ void pers_epilogue_v1(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
                                               int wave, int wm, int wn, int m0, int n0, int tn,
                                               int lane, bool interior) {
   asm volatile("" : "+v"(lane));  // keep lane-derived addresses out of the persistent loop (VGPRs)
+  if constexpr (DBG == 2) {  // ablation: no epilogue at all, accumulators kept live by a dead store
+    float sink = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sink += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (sink == 1234.5f) ((float*)p.C)[lane] = sink;
+    return;
+  }
   const int frow = lane & 15, fg = lane >> 4;
   const EVT_LDS f32x2* coef = (const EVT_LDS f32x2*)(smem + PERS_COEF);
   const EVT_LDS float* colb = (const EVT_LDS float*)(smem + PERS_COLB);
@@ -1087,6 +1098,241 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
   }
 }
 
+// Buffer resource of one tile's rows of an output / residual matrix [M][ld] (bf16): base = the
+// tile's first element (m0, n0), num_records = the bytes to the end of the tile's last valid row,
+// so rows past M are dropped (stores) / read as 0 (loads) by the hardware range check instead of
+// per-lane branches. m0 / n0 go through readfirstlane and every input stays 32-bit: a 64-bit
+// min/max in the byte count is lowered to VALU, and hipcc then no longer proves the descriptor
+// wave-uniform and wraps every buffer op in a waterfall loop (guide T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* mat, int64_t ld, int M,
+                                                           int m0, int n0) {
+  m0 = __builtin_amdgcn_readfirstlane(m0);
+  n0 = __builtin_amdgcn_readfirstlane(n0);
+  const int nr = (min(M - m0, 256) * (int)ld - n0) * 2;  // ld < 2^22: a tile spans < 2 GB
+  return __builtin_amdgcn_make_buffer_rsrc((char*)const_cast<void*>(mat) + ((int64_t)m0 * ld + n0) * 2,
+                                           0, nr, 0x00020000);
+}
+
+// Epilogue of one 256 x 256 tile straight from the accumulators (VALU-bound: every instruction
+// here is paid with the MFMA pipe idle, so the arithmetic is in packed form throughout):
+//   LNIN   r (acc - mu colsum) + c      2 v_pk_fma per column pair
+//   BIAS   acc + bias (+ beta of the residual LayerNorm when RESLN: folded into one add)
+//   RESLN  + gamma (r resid - r mu)     2 v_pk_fma per pair on the unpacked bf16 residual
+//   STATS  (sum, sumsq) of the stored bf16 values with v_dot2c_f32_bf16 (2 per stored dword)
+// Residual loads and output stores go through tile buffer resources (SGPR base per tile, lane
+// offsets tile-invariant, row offsets in SGPRs): no per-store 64-bit address arithmetic and no
+// exec-mask branches for the M edge.
+template <int FL, int DBG = 0, bool PADN = true>
+__device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
+                                              int wave, int wm, int wn, int m0, int n0, int tn,
+                                              int lane, bool interior) {
+  asm volatile("" : "+v"(lane));  // keep lane-derived addresses out of the persistent loop (VGPRs)
+  if constexpr (DBG == 2) {  // ablation: no epilogue at all, accumulators kept live by a dead store
+    float sink = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sink += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (sink == 1234.5f) ((float*)p.C)[lane] = sink;
+    return;
+  }
+  const int frow = lane & 15, fg = lane >> 4;
+  const EVT_LDS f32x2* coef = (const EVT_LDS f32x2*)(smem + PERS_COEF);
+  const EVT_LDS float* colb = (const EVT_LDS float*)(smem + PERS_COLB);
+  auto padskip = [&](int nt) { return PADN && !interior && n0 + wn * 64 + nt * 16 >= p.N; };
+  // 1. MFMA layout: row wm*128 + mt*16 + frow, columns wn*64 + nt*16 + 4 fg + j
+  if constexpr ((FL & EPI_LNIN) != 0) {
+    f32x4 b4[4], c4[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int c = wn * 64 + nt * 16 + 4 * fg;
+      b4[nt] = (FL & EPI_BIAS) ? lds4(colb + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      c4[nt] = lds4(colb + 256 + c);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const f32x2 cf = coef[wm * 128 + mt * 16 + frow];
+      const f32x2 nmu = {-cf[0], -cf[0]}, rr = {cf[1], cf[1]};
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        if (padskip(nt)) continue;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          f32x2 a = {acc[nt][mt][2 * h], acc[nt][mt][2 * h + 1]};
+          const f32x2 cs = {c4[nt][2 * h], c4[nt][2 * h + 1]}, bb = {b4[nt][2 * h], b4[nt][2 * h + 1]};
+          a = __builtin_elementwise_fma(cs, nmu, a);
+          a = __builtin_elementwise_fma(a, rr, bb);
+          acc[nt][mt][2 * h] = a[0];
+          acc[nt][mt][2 * h + 1] = a[1];
+        }
+      }
+    }
+  } else if constexpr ((FL & EPI_BIAS) != 0) {
+    f32x4 b4[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int c = wn * 64 + nt * 16 + 4 * fg;
+      b4[nt] = lds4(colb + c);
+      if (FL & EPI_RESLN) b4[nt] += lds4(colb + 512 + c);  // + beta of LN(resid)
+    }
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        if (padskip(nt)) continue;
+        acc[nt][mt] += b4[nt];
+      }
+  }
+  if constexpr ((FL & (EPI_GELU | EPI_GELU_ERF)) != 0) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      // column group past N (padding of the packed width): wave-uniform skip of the VALU work
+      if (padskip(nt)) continue;
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) acc[nt][mt] = gelu4(acc[nt][mt], (FL & EPI_GELU) ? 0 : 2);
+    }
+  }
+  // 2. store layout: pair (2k, 2k+1) -> lane row wm*128 + (2k + (fg & 1))*16 + frow, columns
+  //    wn*64 + nt*16 + (fg >> 1)*8 + [acc[nt][2k][0..3], acc[nt][2k+1][0..3]]
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) swap_rows16(acc[nt][2 * k], acc[nt][2 * k + 1]);
+  const int rl = wm * 128 + (fg & 1) * 16 + frow;  // + 32 k
+  const int cl = wn * 64 + (fg >> 1) * 8;           // + 16 nt
+  bool cok[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) cok[nt] = !PADN || interior || n0 + cl + 16 * nt < p.N;
+  // 3. residual (16-B buffer loads in the store layout, all issued up front), bf16 stores and the
+  //    row statistics of the stored values; nt-major so each column-vector slice is read once
+  u32x4 rr[4][4];
+  if constexpr ((FL & EPI_RESID) != 0) {
+    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(p.resid, p.ldr, p.M, m0, n0);
+    const int vo = (rl * (int)p.ldr + cl) * 2;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int so = __builtin_amdgcn_readfirstlane(32 * k * (int)p.ldr * 2);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        rr[k][nt] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 32 * nt, so, 0));
+    }
+  }
+  f32x2 rc[4], st[4];
+  u32x4 ov[4][4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    rc[k] = (FL & EPI_RESLN) ? coef[rl + 32 * k] : f32x2{0.f, 0.f};
+    st[k] = f32x2{0.f, 0.f};
+  }
+  const bf16x2 one2 = {(bf16)1.0f, (bf16)1.0f};
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int c = cl + 16 * nt;
+    f32x4 g[2];
+    if (FL & EPI_RESLN) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) g[h] = lds4(colb + 256 + c + 4 * h);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f32x4 v[2] = {acc[nt][2 * k], acc[nt][2 * k + 1]};
+      if constexpr ((FL & EPI_RESID) != 0) {
+        const bf16x8 r8 = __builtin_bit_cast(bf16x8, rr[k][nt]);
+        const f32x2 rrow = {rc[k][1], rc[k][1]}, nrm = {-rc[k][1] * rc[k][0], -rc[k][1] * rc[k][0]};
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const f32x2 rv = {(float)r8[4 * h + 2 * q], (float)r8[4 * h + 2 * q + 1]};
+            f32x2 a = {v[h][2 * q], v[h][2 * q + 1]};
+            if (FL & EPI_RESLN) {  // + gamma (r resid - r mu)   (beta already in the bias)
+              const f32x2 t = __builtin_elementwise_fma(rrow, rv, nrm);
+              a = __builtin_elementwise_fma(f32x2{g[h][2 * q], g[h][2 * q + 1]}, t, a);
+            } else {
+              a += rv;
+            }
+            v[h][2 * q] = a[0];
+            v[h][2 * q + 1] = a[1];
+          }
+      }
+      const bf16x8 o = {(bf16)v[0][0], (bf16)v[0][1], (bf16)v[0][2], (bf16)v[0][3],
+                        (bf16)v[1][0], (bf16)v[1][1], (bf16)v[1][2], (bf16)v[1][3]};
+      ov[k][nt] = __builtin_bit_cast(u32x4, o);
+      if (FL & EPI_STATS) {
+        if (cok[nt]) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            // (from the bf16x8, not bit_cast(bf16x2, ov[k][nt][e]): hipcc 7.2 then feeds word 0
+            // to all four dot2s)
+            const bf16x2 w = {o[2 * e], o[2 * e + 1]};
+            st[k][0] = __builtin_amdgcn_fdot2_f32_bf16(w, one2, st[k][0], false);
+            st[k][1] = __builtin_amdgcn_fdot2_f32_bf16(w, w, st[k][1], false);
+          }
+        }
+      }
+    }
+  }
+  // 4. output: per row pair k, the wave's 32 x 64 block goes through its private 4 KiB of LDS
+  //    (free during the epilogue: buffer-1 regions 2 / 3 are only DMA'd in the next tile's
+  //    phases 1 / 2) and leaves as whole 128-B row segments, 8 rows per store instruction
+  {
+    const int w = wave;
+    EVT_LDS char* scr = (EVT_LDS char*)smem +
+                        (w < 4 ? (96 + 4 + 8 * w) * 1024 : (72 + (w - 4) * 4 + ((w - 4) >> 1) * 8) * 1024);
+    const int wrow = (fg & 1) * 16 + frow;               // store-layout row within the pair
+    const int rrow = lane >> 3, rch = lane & 7;          // row-layout lane: row i*8 + rrow, chunk
+    const bool rcol_ok = !PADN || interior || n0 + wn * 64 + rch * 8 < p.N;
+    const __amdgpu_buffer_rsrc_t cs = tile_rsrc(p.C, p.ldc, p.M, m0, n0);
+    const int vo = ((wm * 128 + rrow) * (int)p.ldc + wn * 64 + rch * 8) * 2;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int ch = 2 * nt + (fg >> 1);
+        *(EVT_LDS u32x4*)(scr + wrow * 128 + ((ch ^ (wrow & 7)) << 4)) = ov[k][nt];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = i * 8 + rrow;
+        const u32x4 v = *(const EVT_LDS u32x4*)(scr + r * 128 + ((rch ^ (r & 7)) << 4));
+        bool keep = rcol_ok;
+        if (DBG == 1) {  // ablation: no stores, every value stays live
+          keep = (v[0] ^ v[1] ^ v[2] ^ v[3]) == 0x12345u;
+        }
+        const int so = __builtin_amdgcn_readfirstlane((32 * k + 8 * i) * (int)p.ldc * 2);
+        if (keep)  // nontemporal (aux nt): whole lines streamed past L2
+          __builtin_amdgcn_raw_buffer_store_b128(v, cs, vo, so, 2);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  }
+  if constexpr ((FL & EPI_STATS) != 0) {
+    // lanes fg and fg ^ 2 hold the two 32-column halves of the same row
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      st[k][0] += __shfl_xor(st[k][0], 32, 64);
+      st[k][1] += __shfl_xor(st[k][1], 32, 64);
+    }
+    EVT_LDS f32x2* part = (EVT_LDS f32x2*)(smem + PERS_PART) + (wn >> 1) * 256;
+    if ((wn & 1) && lane < 32) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) part[rl + 32 * k] = st[k];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    big8_bar();
+    if (!(wn & 1) && lane < 32) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int m = m0 + rl + 32 * k;
+        const f32x2 o = part[rl + 32 * k];
+        if (interior || m < p.M)
+          *(f32x2*)(p.stats_out + 2 * ((int64_t)p.nslots * m + 2 * tn + (wn >> 1))) = st[k] + o;
+      }
+    }
+  }
+}
+
 template <int FL, int DBG = 0, bool PADN = true>
 __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int total) {
   __shared__ __attribute__((aligned(16))) char smem[PERS_LDS];
@@ -1138,11 +1384,14 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
     __builtin_amdgcn_sched_barrier(0);
     stamp(2);
     const bool interior = (m0 + BIG_BM <= p.M) && (n0 + BIG_BN <= p.N);
-    pers_epilogue<FL, DBG, PADN>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior);
+    if constexpr (DBG == 6)  // A/B: the round-1 epilogue
+      pers_epilogue_v1<FL, 0, PADN>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior);
+    else
+      pers_epilogue<FL, DBG, PADN>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior);
     stamp(3);
     ++iter;
     if (!has_next) break;
-    if (!interior || DBG == 1) wait_vmcnt0();
+    if (!interior || DBG == 1 || DBG == 2) wait_vmcnt0();
     tile = next;
     tm = ntm;
     tn = ntn;
@@ -1335,7 +1584,7 @@ constexpr bool pers_fl(int fl) {
 
 // persistent kernel: supported epilogue, 8-column output groups, LN rows of <= 8 slots
 bool use_pers(const GemmParams& p, int flags) {
-  if (g_gemm_variant != 0 && (g_gemm_variant < 9 || g_gemm_variant > 16 || g_gemm_variant == 12 ||
+  if (g_gemm_variant != 0 && (g_gemm_variant < 9 || g_gemm_variant > 19 || g_gemm_variant == 12 ||
                               g_gemm_variant == 14))
     return false;
   if (p.N % 8 || p.vec_ok < 2) return false;
@@ -1358,6 +1607,13 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 3>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 15)  // timeline probe + staggered block start
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 5>), dim3(G), dim3(512), 0, s, q, total);
+  else if (g_gemm_variant == 19)  // A/B: round-1 epilogue
+    hipLaunchKernelGGL((gemm_pers_kernel<FL, 6, false>), dim3(G), dim3(512), 0, s, q, total);
+  else if (g_gemm_variant == 17)  // ablation: main loop + tile loop only (no epilogue)
+    hipLaunchKernelGGL((gemm_pers_kernel<FL, 2, false>), dim3(G), dim3(512), 0, s, q, total);
+  else if (g_gemm_variant == 18)  // ablation: epilogue without the GELU
+    hipLaunchKernelGGL((gemm_pers_kernel<(FL & ~(EPI_GELU | EPI_GELU_ERF)), 0, false>), dim3(G),
+                       dim3(512), 0, s, q, total);
   else if (p.N % BIG_BN == 0)
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 0, false>), dim3(G), dim3(512), 0, s, q, total);
   else

@@ -124,7 +124,7 @@ int evt_model_destroy(evt_model* model);
  * stream-K persistent kernel when there are at least #CUs tiles, else the tile-persistent one),
  * 1 = always 128x128, 2 / 6 / 8 = 256x256 tiles with the plain / interleaved / 8-phase ping-pong
  * main loop whenever the packed width allows (and the output rows are 16-B aligned for bf16),
- * 9 = tile-persistent kernel (no stream-K), 16 = stream-K where it applies; 10-15 and 106 / 108
+ * 9 = tile-persistent kernel (no stream-K), 16 = stream-K where it applies; 10-15, 17-19 and 106 / 108
  * are diagnostic builds (timeline stamps, main loop only). */
 int evt_set_gemm_variant(int variant);
 
