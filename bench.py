@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-probe", action="store_true", help="skip the per-kernel probe")
     ap.add_argument("--gemm-variant", type=int, default=0, help="evt_set_gemm_variant (tuning A/B)")
+    ap.add_argument("--fusion", type=int, default=0,
+                    help="evt_set_fusion flags (0 = separate kernels, 1 = fused QKV + attention)")
     ap.add_argument("--probe-only", type=int, default=0, metavar="N",
                     help="only launch the FC1 probe kernel N times and exit (PMC collection)")
     return ap.parse_args()
@@ -187,6 +189,9 @@ def main():
     else:
         from edgevisiontransformer_amd.modeling.models import vit as mod
     model = mod.build_named(args.model, dtype=args.dtype, seed=0, max_batch=args.batch)
+    if args.fusion:
+        from edgevisiontransformer_amd import _lib
+        _lib.check(_lib.load_library().evt_set_fusion(args.fusion))
     if args.gemm_variant:
         from edgevisiontransformer_amd import _lib
         _lib.check(_lib.load_library().evt_set_gemm_variant(args.gemm_variant))

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libevt_hip.so")
 OBJ = os.path.join(HERE, "build_obj")
-SOURCES = ["gemm.hip", "attention.hip", "norm.hip", "t2t.hip", "swin.hip", "mx8.hip", "capi.cpp"]
+SOURCES = ["gemm.hip", "attention.hip", "qkv_attn.hip", "norm.hip", "t2t.hip", "swin.hip", "mx8.hip", "capi.cpp"]
 HEADERS = ["common.h", "evt_internal.h", os.path.join("..", "..", "include", "evt.h")]
 ARCH = os.environ.get("EVT_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
@@ -27,6 +27,9 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-re
 # (v_accvgpr_read) before the softmax / GELU VALU work (96 copies per window-attention wave).
 PER_FILE_FLAGS = {s: ["-mllvm", "-amdgpu-mfma-vgpr-form=true"]
                   for s in ("attention.hip", "swin.hip", "t2t.hip")}
+# qkv_attn.hip: no NaN operands on the path, so fmaxf on raw MFMA results needs no canonicalising
+# v_max per element before the softmax max tree (-inf masking is unaffected)
+PER_FILE_FLAGS["qkv_attn.hip"] = ["-fno-honor-nans"]
 
 
 def _hipcc() -> str:

@@ -153,6 +153,9 @@ struct evt_model {
 
 namespace {
 
+int g_fusion = 0;  // evt_set_fusion (opt-in: the fused kernel is slower today)
+bool fused_attention_enabled() { return (g_fusion & EVT_FUSE_QKV_ATTENTION) != 0; }
+
 int dev_alloc(evt_model* m, void** p, size_t bytes) {
   if (bytes == 0) bytes = 16;
   hipError_t e = hipMalloc(p, bytes);
@@ -412,16 +415,28 @@ int alloc_encoder_ws(evt_model* m, int B, size_t hbuf_bytes, hipStream_t s) {
 int run_encoder(evt_model* m, int B, hipStream_t s) {
   const int D = m->D, T = m->sh.T, rows = B * T;
   const float log2e = 1.4426950408889634f;
+  const bool fuse = m->dtype == DT_BF16 && D % 64 == 0 && qkv_attn_supported(T, D) &&
+                    fused_attention_enabled();
   for (const Layer& L : m->layers) {
-    {  // LN1-folded QKV (attention.py:24)
-      DenseCall c;
-      c.flags = EPI_LNIN | EPI_BIAS;
-      c.A = m->x; c.lda = D; c.C = m->qkv; c.ldc = 3 * L.inner; c.M = rows; c.N = 3 * L.inner;
-      c.stats_in = m->sx;
-      EVT_RC(dense(m, L.qkv, c, s));
+    if (fuse) {  // LN1-folded QKV + attention in one kernel (qkv_attn.hip)
+      QkvAttnParams p{};
+      p.x = m->x; p.ldx = D; p.stats = m->sx; p.nslots = stats_slots(D);
+      p.inv_d = 1.0f / (float)D; p.eps = m->eps;
+      p.W = L.qkv.w; p.ldw = L.qkv.kpad; p.colsum = L.qkv.colsum; p.cvec = L.qkv.b; p.K = L.qkv.kpad;
+      p.inner = L.inner; p.H = L.heads; p.N = T; p.B = B;
+      p.out = m->o; p.ldo = L.inner; p.scale_log2 = 0.125f * log2e;
+      EVT_HIP(qkv_attn_launch(p, s), "qkv_attention");
+    } else {
+      {  // LN1-folded QKV (attention.py:24)
+        DenseCall c;
+        c.flags = EPI_LNIN | EPI_BIAS;
+        c.A = m->x; c.lda = D; c.C = m->qkv; c.ldc = 3 * L.inner; c.M = rows; c.N = 3 * L.inner;
+        c.stats_in = m->sx;
+        EVT_RC(dense(m, L.qkv, c, s));
+      }
+      AttnParams ap{m->qkv, 3 * L.inner, m->o, L.inner, T, L.heads, B, 0.125f * log2e};
+      EVT_HIP(attention_launch(m->dtype, ap, s), "attention");
     }
-    AttnParams ap{m->qkv, 3 * L.inner, m->o, L.inner, T, L.heads, B, 0.125f * log2e};
-    EVT_HIP(attention_launch(m->dtype, ap, s), "attention");
     {  // out-proj + bias + LN1(x) residual -> xm (+ stats); STANDARD: + x
       DenseCall c;
       c.flags = m->standard ? (EPI_BIAS | EPI_RESID | EPI_STATS)
@@ -1207,6 +1222,12 @@ int evt_patch_merge(int dtype, const void* x, int64_t ldx, int B, int R, int C, 
 
 // ---- op-level entry points --------------------------------------------------------------
 
+int evt_set_fusion(int flags) {
+  if (flags & ~EVT_FUSE_QKV_ATTENTION) return fail(EVT_EINVAL, "unknown fusion flag");
+  g_fusion = flags;
+  return EVT_OK;
+}
+
 int evt_set_gemm_variant(int variant) {
   if (variant != 0 && variant != 1 && variant != 2 && variant != 6 && variant != 8 &&
       !(variant >= 9 && variant <= 19) && variant != 106 && variant != 108)
@@ -1362,6 +1383,22 @@ int evt_attention(int dtype, const void* qkv, int64_t ldq, void* out, int64_t ld
     return fail(EVT_EINVAL, "attention: bad shape (N <= 256, head size 64)");
   AttnParams p{qkv, ldq, out, ldo, N, H, B, scale * 1.4426950408889634f};
   EVT_HIP(attention_launch(dtype, p, (hipStream_t)stream), "attention");
+  return EVT_OK;
+}
+
+int evt_qkv_attention(const void* x, int D, const float* stats, const void* Wp, const float* colsum,
+                      const float* cvec, int B, int N, int H, float scale, float eps, void* out,
+                      int64_t ldo, void* stream) {
+  if (!x || !stats || !Wp || !colsum || !cvec || !out || B < 0 || H <= 0 || D <= 0 || D % 64 ||
+      !qkv_attn_supported(N, D) || ldo < H * 64)
+    return fail(EVT_EINVAL, "qkv_attention: bad shape (192 < N <= 208, D % 64 == 0, head size 64)");
+  QkvAttnParams p{};
+  p.x = x; p.ldx = D; p.stats = stats; p.nslots = stats_slots(D);
+  p.inv_d = 1.0f / (float)D; p.eps = eps;
+  p.W = Wp; p.ldw = D; p.colsum = colsum; p.cvec = cvec; p.K = D;
+  p.inner = H * 64; p.H = H; p.N = N; p.B = B;
+  p.out = out; p.ldo = ldo; p.scale_log2 = scale * 1.4426950408889634f;
+  EVT_HIP(qkv_attn_launch(p, (hipStream_t)stream), "qkv_attention");
   return EVT_OK;
 }
 

@@ -84,6 +84,26 @@ struct AttnParams {
 };
 hipError_t attention_launch(int dtype, const AttnParams& p, hipStream_t s);
 
+// Fused LN1-folded QKV projection + attention (qkv_attn.hip, bf16): x rows [B*N][ldx] raw token
+// stream, stats [B*N][nslots][2] its slab statistics, W the packed LN-folded Wqkv (rows (qkv h d),
+// ldw = K = Kpad), colsum / cvec per packed row; O rows [B*N][ldo], columns (h d).
+struct QkvAttnParams {
+  const void* x; int64_t ldx;
+  const float* stats; int nslots;
+  float inv_d, eps;
+  const void* W; int64_t ldw;
+  const float* colsum; const float* cvec;
+  int K;          // Kpad: multiple of 64 (the x rows are read up to K: ldx >= K, zero padded)
+  int inner;      // H * 64
+  int H, N, B;
+  void* out; int64_t ldo;
+  float scale_log2;
+  int dbg;        // diagnostic ablations (EVT_QA_DBG): 1 no attention, 2 main loop only,
+                  // 3 one workgroup per CU
+};
+bool qkv_attn_supported(int N, int K);
+hipError_t qkv_attn_launch(const QkvAttnParams& p, hipStream_t s);
+
 // LayerNorm over rows of D (fp32 in) -> activation dtype out (eps 1e-5).
 hipError_t layernorm_launch(int dtype, const float* x, int64_t ldx, void* y, int64_t ldy,
                             const float* gamma, const float* beta, int rows, int D, float eps,

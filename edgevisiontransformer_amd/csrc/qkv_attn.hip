@@ -1,0 +1,446 @@
+// Fused LN1-folded QKV projection + multi-head self-attention for the ViT encoder on gfx950.
+//
+// Replaces, per encoder layer, the QKV Dense of the pre-norm attention sublayer (reference
+// `modeling/layers/norm.py:12` LayerNorm + `modeling/layers/attention.py:17,24` to_qkv) AND the
+// attention core (`attention.py:20-34`: the (qkv h d) split, q.k^T * h_k^-0.5, softmax, attn.v,
+// 'b h n d -> b n (h d)'), so that q / k / v never leave the CU: the unfused path writes the
+// [B*N, 3*H*64] qkv matrix to HBM and reads it back (930 MB per layer at DeiT-base bs512).
+//
+// Work item = (image b, head h): a 208 x 192 GEMM tile C = LN1(x_b) . W[:, q|k|v of head h]
+// (K = D), then that head's attention out of LDS. One 4-wave workgroup per item, two per CU
+// (81 664 B of LDS each).
+//
+// Status (DESIGN.md "Fused QKV + attention"): correct, but slower than the separate LN-folded QKV
+// GEMM + attention kernels at DeiT-base bs512 (515 vs 485 us per layer): this 208 x 192, K-tile
+// 32 main loop alone takes ~365 us where the 256 x 256 8-phase persistent GEMM needs 281 us for
+// the same product, and the attention phase (~110 us) is not hidden by the co-resident workgroup.
+// Opt-in through evt_set_fusion(EVT_FUSE_QKV_ATTENTION).
+//
+// GEMM (as gemm.hip): transposed product C^T = W . x^T on v_mfma_f32_16x16x32_bf16 (lane: token
+// row t*16 + (lane & 15), features 4 (lane >> 4) + j), both operands K-contiguous and staged by
+// global_load_lds into a three-buffer ring of [208 token rows | 192 weight rows] x 64 B (K-tiles
+// of 32; chunk ^ ((row >> 1) & 3) swizzle on the source address and on every fragment read:
+// conflict-free for the ds_read_b128 lane groups), one K-tile in flight across each barrier
+// (counted vmcnt). The LayerNorm is folded as in the GEMM (v = r (acc - mu colsum) + c, the
+// packed weights carrying gamma): the raw token stream and its slab statistics are the inputs.
+//
+// Wave roles: wave w computes all 12 feature tiles (q 0-3, k 4-7, v 8-11) of token tiles w,
+// w + 4, w + 8 and feature tiles 3 w .. 3 w + 2 of token tile 12 (39 MFMA columns per K-tile for
+// every wave; per K-tile 4 token + 12 weight fragment reads: one weight fragment feeds 3-4 MFMAs).
+// Epilogue: K and V (bf16) go to LDS; Q stays in registers as the B operand of S^T = K Q^T (token
+// tile 12's Q, split over the waves, goes through a 2 KB LDS tile). The
+// head feature d is permuted inside each 32-wide k-step so that the accumulator layout IS that
+// operand: k-step s, lane group g, element e <-> d = 16 (2 s + (e >> 2)) + 4 g + (e & 3); K rows
+// are written to LDS in the same permuted order (the dot product is order-free). V keeps natural
+// order (its d is the output feature) and is read transposed (ds_read_b64_tr_b16).
+// Attention: wave w handles its q tiles as attention.hip does (exact softmax over all keys in
+// registers, O^T = V^T P^T with P^T the converted S^T accumulator), the row max / sum as balanced
+// trees, the scale folded into the exponent.
+#include <cstdlib>
+
+#include "common.h"
+#include "evt_internal.h"
+
+namespace evt {
+
+namespace {
+
+constexpr int QA_NT = 13;                           // 16-token tiles per image (N in (192, 208])
+constexpr int QA_ROWS = QA_NT * 16;                 // 208
+constexpr int QA_SRB = 64;                          // staging row bytes (32 k)
+constexpr int QA_XT = QA_ROWS * QA_SRB;             // 13,312: token rows of one K-tile
+constexpr int QA_WT = 192 * QA_SRB;                 // 12,288: weight rows (q k v of the head)
+constexpr int QA_STAGE = QA_XT + QA_WT;             // 25,600
+constexpr int QA_NSTAGE = 3;
+constexpr int QA_RB = 128;                          // K / V rows: 64 d bf16
+constexpr int QA_KVB = QA_ROWS * QA_RB;             // 26,624: K or V
+constexpr int QA_Q12 = 2 * QA_KVB;                  // token tile 12's Q (16 rows, permuted d)
+constexpr int QA_COEF = QA_NSTAGE * QA_STAGE;       // [208] {-mu, -mu, r, r} after the ring
+constexpr int QA_VEC = QA_COEF + QA_ROWS * 16;      // [192] colsum, [192] c
+constexpr int QA_LDS = QA_VEC + 192 * 8;            // 81,664
+static_assert(QA_Q12 + 16 * QA_RB <= QA_COEF, "K / V / Q12 overlay the staging ring");
+static_assert(2 * QA_LDS <= 160 * 1024, "two workgroups per CU");
+constexpr int QA_PIECES = 7;  // glds per wave per K-tile (13 token + 12 weight pieces; waves
+                              // 1-3 repeat token piece 12 so that every count is the same)
+
+__device__ __forceinline__ int qa_remap(int bid, int nwg) {  // XCD-aware (gemm.hip xcd_remap)
+  const int xcd = bid & 7, local = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
+}
+
+// Workgroup barrier that memory operations cannot cross (s_barrier alone is "no memory" to the
+// compiler, which may then hoist a staging-buffer ds_read above it: a race with other waves' DMA).
+__device__ __forceinline__ void qa_bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void mma(const u32x4& a, const u32x4& b, f32x4& c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                              __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+// LN fold of one accumulator quad (features n..n+3 of a token row): v = r (acc - mu colsum) + c,
+// the persistent GEMM's EPI_LNIN arithmetic; cf = {-mu, -mu, r, r} as stored per token, so that
+// both packed FMAs take register pairs as they are. (With (mu, r) broadcast into the pairs by
+// op_sel, v_pk_fma_f32 produced wrong low halves in lanes 48-63 whenever two of these workgroups
+// shared a CU - measured: the raw accumulators were right, the folded values not.)
+__device__ __forceinline__ f32x4 qa_fold(f32x4 a, f32x4 cf, f32x4 cs, f32x4 cc) {
+  const f32x2 nmu = {cf[0], cf[1]}, rr = {cf[2], cf[3]};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    f32x2 v = {a[2 * h], a[2 * h + 1]};
+    v = __builtin_elementwise_fma(f32x2{cs[2 * h], cs[2 * h + 1]}, nmu, v);
+    v = __builtin_elementwise_fma(v, rr, f32x2{cc[2 * h], cc[2 * h + 1]});
+    a[2 * h] = v[0];
+    a[2 * h + 1] = v[1];
+  }
+  return a;
+}
+
+__device__ __forceinline__ u32x2 pack4(f32x4 v) {
+  const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+  return __builtin_bit_cast(u32x2, o);
+}
+
+// S^T = K Q^T of one 16-query tile (K in the permuted-d LDS image; the K fragments are read per
+// call: kept from being hoisted out of the caller's tile loop, 104 VGPRs).
+__device__ __forceinline__ void qa_scores(const EVT_LDS char* Ks, u32x4 qf0, u32x4 qf1,
+                                          f32x4 (&s)[QA_NT], int lane) {
+  asm volatile("" : "+v"(lane));
+  const int g = lane >> 4, c16 = lane & 15, sw = lane & 7;
+#pragma unroll
+  for (int kt = 0; kt < QA_NT; ++kt) {
+    const EVT_LDS char* kr = Ks + (kt * 16 + c16) * QA_RB;
+    const u32x4 k0 = *(const EVT_LDS u32x4*)(kr + ((g ^ sw) * 16));
+    const u32x4 k1 = *(const EVT_LDS u32x4*)(kr + (((g + 4) ^ sw) * 16));
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    mma(k0, qf0, acc);
+    mma(k1, qf1, acc);
+    s[kt] = acc;
+  }
+}
+
+// Softmax of one tile (row max / sum as balanced trees; the h_k^-0.5 log2 e scale folded into the
+// exponent: exp2(s c - max c), valid as c > 0), O^T = V^T P^T, the bf16 stores.
+__device__ __forceinline__ void qa_finish(const QkvAttnParams& p, const EVT_LDS char* Vs,
+                                          f32x4 (&s)[QA_NT], int qt, int64_t row0, int head,
+                                          int lane) {
+  constexpr int NKT = QA_NT, ROWB = QA_RB;
+  const int g = lane >> 4, c16 = lane & 15;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if ((NKT - 1) * 16 + 4 * g + j >= p.N) s[NKT - 1][j] = -INFINITY;
+  float m[16];
+#pragma unroll
+  for (int kt = 0; kt < 16; ++kt)
+    m[kt] = kt < NKT ? fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3])) : -INFINITY;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) m[i] = fmaxf(m[2 * i], m[2 * i + 1]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) m[i] = fmaxf(m[2 * i], m[2 * i + 1]);
+  m[0] = fmaxf(fmaxf(m[0], m[1]), fmaxf(m[2], m[3]));
+  float mx = m[0];
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  const f32x2 sc2 = {p.scale_log2, p.scale_log2};
+  const f32x2 mo2 = {-mx * p.scale_log2, -mx * p.scale_log2};
+  f32x2 t[16];
+#pragma unroll
+  for (int kt = 0; kt < 16; ++kt) {
+    if (kt >= NKT) {
+      t[kt] = f32x2{0.f, 0.f};
+      continue;
+    }
+    f32x2 e[2];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      f32x2 v = {s[kt][2 * hh], s[kt][2 * hh + 1]};
+      v = __builtin_elementwise_fma(v, sc2, mo2);
+      e[hh] = f32x2{__builtin_amdgcn_exp2f(v[0]), __builtin_amdgcn_exp2f(v[1])};
+      s[kt][2 * hh] = e[hh][0];
+      s[kt][2 * hh + 1] = e[hh][1];
+    }
+    t[kt] = e[0] + e[1];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) t[i] = t[2 * i] + t[2 * i + 1];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) t[i] = t[2 * i] + t[2 * i + 1];
+  t[0] = (t[0] + t[1]) + (t[2] + t[3]);
+  float sum = t[0][0] + t[0][1];
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int vl = lane;
+  asm volatile("" : "+v"(vl));  // (V^T fragments: not hoisted out of the tile loop either)
+  const int tq = (vl >> 2) & 3, tp = vl & 3;
+#pragma unroll
+  for (int ks = 0; ks < (NKT + 1) / 2; ++ks) {
+    const bool half = (NKT % 2) && ks == NKT / 2;  // last 16 keys: the upper k half is zero
+    bf16x8 pf;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pf[j] = (bf16)s[2 * ks][j];
+      pf[4 + j] = half ? (bf16)0.f : (bf16)s[half ? 0 : 2 * ks + 1][j];
+    }
+    const int key0 = ks * 32 + 4 * (vl >> 4) + tq;  // key0 & 7 == key1 & 7
+    const int ksw = key0 & 7;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int chunk = 2 * dt + (tp >> 1);
+      const int off = ((chunk ^ ksw) * 16) + (tp & 1) * 8;
+      const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((EVT_LDS i16x4*)(Vs + key0 * ROWB + off));
+      i16x4 v1 = {0, 0, 0, 0};
+      if (!half)
+        v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((EVT_LDS i16x4*)(Vs + (key0 + 16) * ROWB + off));
+      const i16x8 vv = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[dt],
+                                                      0, 0, 0);
+    }
+  }
+  const int q = qt * 16 + c16;
+  if (q < p.N) {
+    const f32x4 inv = f32x4{1.f, 1.f, 1.f, 1.f} * __builtin_amdgcn_rcpf(sum);
+    bf16* op = (bf16*)p.out + (row0 + q) * p.ldo + head * 64 + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) store4(op + dt * 16, o[dt] * inv);
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void qkv_attn_kernel(QkvAttnParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // QA_LDS bytes (dynamic)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int item = qa_remap(blockIdx.x, gridDim.x);  // the heads of one image on one XCD
+  const int b = item / p.H, head = item - b * p.H;
+  const int frow = lane & 15, g = lane >> 4;
+  const int fsw = (frow >> 1) & 3;                   // staging swizzle of the fragment rows
+  const int64_t row0 = (int64_t)b * p.N;
+  const int nk = p.K / 32;
+
+  // LayerNorm coefficients of the tile rows and the fold vectors of the head's 192 features
+  // (plain loads, before any global_load_lds is in flight)
+  if (tid < QA_ROWS) {
+    const float* st = p.stats + (row0 + min(tid, p.N - 1)) * 2 * p.nslots;
+    float s1 = 0.f, s2 = 0.f;
+    for (int j = 0; j < p.nslots; ++j) {
+      const f32x2 v = *(const f32x2*)(st + 2 * j);
+      s1 += v[0];
+      s2 += v[1];
+    }
+    const float mu = s1 * p.inv_d;
+    const float r = rsqrtf(fmaxf(s2 * p.inv_d - mu * mu, 0.f) + p.eps);
+    ((EVT_LDS f32x4*)(smem + QA_COEF))[tid] = f32x4{-mu, -mu, r, r};
+  }
+  if (tid < 192) {
+    const int prow = (tid >> 6) * p.inner + head * 64 + (tid & 63);
+    ((EVT_LDS float*)(smem + QA_VEC))[tid] = p.colsum[prow];
+    ((EVT_LDS float*)(smem + QA_VEC))[192 + tid] = p.cvec[prow];
+  }
+
+  // ---- staging: a K-tile is 13 (tokens) + 12 (weights) pieces of 16 rows x 64 B; wave w DMAs
+  // token pieces w, w + 4, w + 8, 12 and weight pieces w, w + 4, w + 8
+  const int srow = lane >> 2, sch = lane & 3;         // piece row, 16-B chunk
+  const int schunk = (sch ^ ((srow >> 1) & 3)) * 16;  // global source chunk of this LDS slot
+  // wave-uniform bases (SGPRs) + 32-bit per-lane offsets
+  const char* xb = (const char*)p.x + row0 * p.ldx * 2;
+  const char* wb = (const char*)p.W + (int64_t)head * 64 * p.ldw * 2;
+  int xo[4], wo[3];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int piece = min(wave + 4 * j, QA_NT - 1);
+    xo[j] = min(piece * 16 + srow, p.N - 1) * (int)p.ldx * 2 + schunk;
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int r = (wave + 4 * j) * 16 + srow;           // 0..191: (q|k|v, d)
+    wo[j] = ((r >> 6) * p.inner + (r & 63)) * (int)p.ldw * 2 + schunk;
+  }
+  auto stage = [&](int kt) {
+    EVT_LDS char* base = (EVT_LDS char*)smem + (kt % QA_NSTAGE) * QA_STAGE;
+    const int koff = kt * 64;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      glds16(xb + (xo[j] + koff), base + min(wave + 4 * j, QA_NT - 1) * 16 * QA_SRB);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) glds16(wb + (wo[j] + koff), base + QA_XT + (wave + 4 * j) * 16 * QA_SRB);
+  };
+
+  // acc[i][f]: token tile w + 4 i, feature tile f; a12[f]: token tile 12, feature tile 3 w + f
+  f32x4 acc[3][12], a12[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int f = 0; f < 12; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int f = 0; f < 3; ++f) a12[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int coff = (g ^ fsw) * 16;
+  auto kstep = [&](int kt) {
+    const EVT_LDS char* Xs = (const EVT_LDS char*)smem + (kt % QA_NSTAGE) * QA_STAGE;
+    const EVT_LDS char* Ws = Xs + QA_XT;
+    // weight fragments: the 12 feature tiles, then the wave's 3 for token tile 12; each read two
+    // fragments ahead of its MFMAs (counted lgkmcnt waits, not a drain per group)
+    auto wfrag = [&](int j) {
+      const int F = j < 12 ? j : 3 * wave + (j - 12);
+      return *(const EVT_LDS u32x4*)(Ws + (F * 16 + frow) * QA_SRB + coff);
+    };
+    u32x4 xf[3], x12;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) xf[i] = *(const EVT_LDS u32x4*)(Xs + ((wave + 4 * i) * 16 + frow) * QA_SRB + coff);
+    x12 = *(const EVT_LDS u32x4*)(Xs + (12 * 16 + frow) * QA_SRB + coff);
+    u32x4 w0 = wfrag(0), w1 = wfrag(1);
+#pragma unroll
+    for (int j = 0; j < 15; ++j) {
+      const u32x4 w2 = j + 2 < 15 ? wfrag(j + 2) : w1;
+      if (j < 12) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) mma(w0, xf[i], acc[i][j]);
+      } else {
+        mma(w0, x12, a12[j - 12]);
+      }
+      w0 = w1;
+      w1 = w2;
+    }
+    // issue order: the 6 first reads, then per step one read (two steps ahead) and its MFMAs
+    __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+  };
+  // main loop: K-tile kt + 1 stays in flight across the barrier of K-tile kt (counted vmcnt)
+  stage(0);
+  if (nk > 1) stage(1);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // QA_PIECES
+    else wait_vmcnt0();
+    qa_bar();
+    if (kt + 2 < nk) stage(kt + 2);  // into the buffer K-tile kt - 1 was read from
+    kstep(kt);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  qa_bar();  // every wave is past its last staging read: K / V may overwrite
+  if (p.dbg == 2) {  // ablation: main loop only (accumulators kept live by a dead store)
+    float sink = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int f = 0; f < 12; ++f) sink += acc[i][f][0];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) sink += a12[f][1];
+    if (sink == 1234.5f) ((float*)p.out)[tid] = sink;
+    return;
+  }
+
+  // ---- epilogue: LN fold; Q of tiles w, w + 4, w + 8 to registers; K / V and tile 12's Q to LDS
+  const EVT_LDS f32x4* coef = (const EVT_LDS f32x4*)(smem + QA_COEF);
+  const EVT_LDS float* vcs = (const EVT_LDS float*)(smem + QA_VEC);
+  const EVT_LDS float* vcc = vcs + 192;
+  EVT_LDS char* Kh = (EVT_LDS char*)smem;
+  EVT_LDS char* Vh = Kh + QA_KVB;
+  EVT_LDS char* Q12 = (EVT_LDS char*)smem + QA_Q12;
+  // LDS byte offset (within a 16-row tile) of this lane's 4 features of feature tile F:
+  // K / Q (F < 8): d = 16 (F & 3) + 4 g + j at the permuted position 32 (F&3 >> 1) + 8 g + 4 (F & 1) + j;
+  // V (F >= 8): natural d = 16 (F - 8) + 4 g + j.
+  auto fdst = [&](int F) {
+    const int Fl = F & 3;
+    const int ch = F < 8 ? 4 * (Fl >> 1) + g : 2 * Fl + (g >> 1);
+    const int hb = F < 8 ? 8 * (Fl & 1) : 8 * (g & 1);
+    return frow * QA_RB + ((ch ^ (frow & 7)) << 4) + hb;
+  };
+  u32x4 qf[3][2];
+  {
+    f32x4 cf[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) cf[i] = coef[(wave + 4 * i) * 16 + frow];
+    u32x2 qv[3][4];
+#pragma unroll
+    for (int f = 0; f < 12; ++f) {  // fold vectors read once per feature tile
+      const int n = f * 16 + 4 * g;
+      const f32x4 cs = *(const EVT_LDS f32x4*)(vcs + n), cc = *(const EVT_LDS f32x4*)(vcc + n);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const u32x2 v = pack4(qa_fold(acc[i][f], cf[i], cs, cc));
+        if (f < 4) qv[i][f] = v;
+        else *(EVT_LDS u32x2*)((f < 8 ? Kh : Vh) + (wave + 4 * i) * 16 * QA_RB + fdst(f)) = v;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        qf[i][s] = u32x4{qv[i][2 * s][0], qv[i][2 * s][1], qv[i][2 * s + 1][0], qv[i][2 * s + 1][1]};
+  }
+  {
+    const f32x4 cf = coef[12 * 16 + frow];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      const int F = 3 * wave + f, n = F * 16 + 4 * g;
+      const u32x2 v = pack4(qa_fold(a12[f], cf, *(const EVT_LDS f32x4*)(vcs + n),
+                                    *(const EVT_LDS f32x4*)(vcc + n)));
+      EVT_LDS char* dst = F < 4 ? Q12 : (F < 8 ? Kh : Vh) + 12 * 16 * QA_RB;
+      *(EVT_LDS u32x2*)(dst + fdst(F)) = v;
+    }
+  }
+  // materialise the Q fragments here: left to itself the compiler sinks their fold past the
+  // barrier into the attention, keeping the fp32 accumulators live there (spills)
+#pragma unroll
+  for (int i = 0; i < 3; ++i) asm volatile("" : "+v"(qf[i][0]), "+v"(qf[i][1]));
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- attention: q tiles w, w + 4, w + 8 (Q in registers); tile 12 by wave head & 3
+  if (p.dbg == 1) {  // ablation: no attention
+    if (qf[0][0][0] == 0x12345u && qf[2][1][3] == 7u) ((unsigned*)p.out)[tid] = qf[1][0][1];
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    f32x4 sc[QA_NT];
+    qa_scores(Kh, qf[i][0], qf[i][1], sc, lane);
+    qa_finish(p, Vh, sc, wave + 4 * i, row0, head, lane);
+    __builtin_amdgcn_sched_barrier(0);  // one tile at a time (register pressure)
+  }
+  if (wave == (head & 3)) {
+    const EVT_LDS char* qr = Q12 + frow * QA_RB;
+    const u32x4 q0 = *(const EVT_LDS u32x4*)(qr + ((g ^ (frow & 7)) * 16));
+    const u32x4 q1 = *(const EVT_LDS u32x4*)(qr + (((g + 4) ^ (frow & 7)) * 16));
+    f32x4 sc[QA_NT];
+    qa_scores(Kh, q0, q1, sc, lane);
+    qa_finish(p, Vh, sc, 12, row0, head, lane);
+  }
+}
+
+}  // namespace
+
+bool qkv_attn_supported(int N, int D) { return N > 192 && N <= QA_ROWS && D % 32 == 0 && D >= 64; }
+
+hipError_t qkv_attn_launch(const QkvAttnParams& p, hipStream_t s) {
+  if (p.B <= 0) return hipSuccess;
+  if (!qkv_attn_supported(p.N, p.K) || p.H <= 0 || p.nslots <= 0) return hipErrorInvalidValue;
+  const int items = p.B * p.H;
+  static const int dbg = [] {
+    const char* e = getenv("EVT_QA_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  QkvAttnParams q = p;
+  q.dbg = dbg;
+  // EVT_QA_DBG 3: 4 KB of dynamic LDS on top (diagnostic: one workgroup per CU)
+  hipLaunchKernelGGL(qkv_attn_kernel, dim3(items), dim3(256), QA_LDS + (dbg == 3 ? 4096 : 0), s, q);
+  return hipGetLastError();
+}
+
+}  // namespace evt

@@ -128,6 +128,13 @@ int evt_model_destroy(evt_model* model);
  * are diagnostic builds (timeline stamps, main loop only). */
 int evt_set_gemm_variant(int variant);
 
+/* Fused-kernel switches (process-wide; default 0 = the separate QKV GEMM + attention kernels):
+ * EVT_FUSE_QKV_ATTENTION runs each bf16 ViT layer's LN1-folded QKV Dense and attention core as
+ * one kernel (evt_qkv_attention) where the token count allows. Opt-in: measured slower than the
+ * separate kernels at DeiT-base bs512 ("Fused QKV + attention"). */
+#define EVT_FUSE_QKV_ATTENTION 1
+int evt_set_fusion(int flags);
+
 /* Pack a Keras [K, N] fp32 kernel into the GEMM operand layout Wp[Npad][Kpad] (dtype), zero
  * padded, optionally scaling row k by row_scale[k] (a LayerNorm gamma folded into the weights;
  * NULL = no scaling). Npad % 128 == 0, Kpad % 64 == 0. */
@@ -178,6 +185,17 @@ typedef struct evt_dense_args {
  * residual + stats); Swin: 289 (LN-folded FC1 + erf GELU), 133 (proj / FC2 + residual + stats),
  * 161 (LN-folded patch-merge reduction + stats). */
 int evt_dense(int dtype, const evt_dense_args* args, void* stream);
+
+/* Fused attention sublayer up to the out-projection (bf16 only): the LN1-folded QKV Dense
+ * (norm.py:12 + attention.py:17,24) and the attention core (attention.py:20-34) in one kernel, q / k
+ * / v never written to memory. x [B*N, D] the raw token stream (bf16, D % 64 == 0), stats
+ * [B*N, 2*ceil(D/256), 2] its per-slab (sum, sum of squares) partials (any split over the slots),
+ * Wp / colsum / cvec the packed gamma-folded Keras [D, 3*H*64] qkv kernel (evt_pack_weight with
+ * row_scale = gamma, Kpad = D) and its fold vectors (evt_ln_fold with beta and the qkv bias or
+ * NULL); out [B*N, ldo] columns (h d). 192 < N <= 208 (the 224/16 ViT token count 197). */
+int evt_qkv_attention(const void* x, int D, const float* stats, const void* Wp, const float* colsum,
+                      const float* cvec, int B, int N, int H, float scale, float eps, void* out,
+                      int64_t ldo, void* stream);
 
 /* Multi-head attention core (attention.py:20-34): qkv [B*N, ldq] with columns (qkv h d), head
  * size 64 -> out [B*N, ldo] columns (h d). N <= 256. */

@@ -27,7 +27,7 @@ def lib():
 def test_header_and_binding_agree():
     from edgevisiontransformer_amd import _lib
     assert _declared() == sorted(_lib.SIGNATURES)
-    assert len(_declared()) == 34
+    assert len(_declared()) == 36
 
 
 def test_every_declared_symbol_is_exported(lib):
@@ -54,6 +54,9 @@ def test_host_validation_codes(lib):
     out_h = ctypes.c_void_p()
     assert lib.evt_vit_create(ctypes.byref(d), None, 0, None, ctypes.byref(out_h)) == _lib.EVT_EINVAL
     assert lib.evt_model_destroy(None) == 0
+    assert lib.evt_set_fusion(99) == _lib.EVT_EINVAL
+    assert lib.evt_set_fusion(_lib.FUSE_QKV_ATTENTION) == 0
+    assert lib.evt_set_fusion(0) == 0
     assert lib.evt_graph_launch(None, None) == _lib.EVT_EINVAL
     assert lib.evt_graph_capture(None, None, 1, None, None) == _lib.EVT_EINVAL
 

@@ -1,0 +1,138 @@
+"""Fused LN1-folded QKV + attention kernel (csrc/qkv_attn.hip, evt_qkv_attention) against
+(a) the fp64 restatement of the reference sublayer up to the out-projection (LayerNorm
+norm.py:12 -> to_qkv attention.py:24 -> attention.py:20-34) on the same bf16 inputs, and
+(b) the unfused GPU path (LN-folded QKV GEMM + attention kernel), whose q / k / v the fused kernel
+reproduces bit for bit before the attention (only the order of the head-feature sum in q.k^T
+differs: results agree to the bf16 rounding of O)."""
+import math
+
+import pytest
+import torch
+
+from edgevisiontransformer_amd import _lib
+from tests import _ops
+from tests.test_gpu_ops import _attn_ref, _ln64, _nslots, _q, _rand
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(gpu, B, N, H, D, bias, seed=0, split_stats=False):
+    x64 = _rand((B * N, D), 61 + seed, 1.3) + 0.3
+    g64, be64 = 1.0 + _rand((D,), 62 + seed, 0.1), _rand((D,), 63 + seed, 0.1)
+    W64 = _rand((D, 3 * H * 64), 64 + seed, 1 / math.sqrt(D))
+    b64 = _rand((3 * H * 64,), 65 + seed, 0.05) if bias else None
+    xq = _q(x64, "bf16")
+    W = W64.float().to(gpu)
+    g, be = g64.float().to(gpu), be64.float().to(gpu)
+    wp, kpad, npad = _ops.pack(W, "bf16", row_scale=g)
+    colsum, cvec = _ops.ln_fold("bf16", wp, kpad, npad, W, be,
+                                b64.float().to(gpu) if bias else None)
+    S = _nslots(D)
+    st = torch.zeros((B * N, S, 2), dtype=torch.float32)
+    xf = xq.float()
+    if split_stats:  # partials spread over the slots, as the GEMM epilogues write them
+        parts = torch.tensor_split(xf, S, dim=1)
+        for j, pj in enumerate(parts):
+            st[:, j, 0], st[:, j, 1] = pj.sum(-1), (pj * pj).sum(-1)
+    else:
+        st[:, 0, 0], st[:, 0, 1] = xf.sum(-1), (xf * xf).sum(-1)
+    x = xq.to(torch.bfloat16).to(gpu)
+    stats = st.to(gpu)
+    return x, stats, wp, kpad, npad, colsum, cvec, xq, g64, be64, W64, b64
+
+
+@pytest.mark.parametrize("B,N,H,D,bias", [(2, 197, 12, 768, False), (3, 197, 3, 192, True),
+                                          (1, 197, 6, 384, False), (2, 200, 5, 320, True),
+                                          (1, 208, 2, 64, False), (4, 193, 1, 128, False)])
+def test_qkv_attention_vs_fp64(gpu, B, N, H, D, bias):
+    x, stats, wp, kpad, npad, colsum, cvec, xq, g64, be64, W64, b64 = _case(gpu, B, N, H, D, bias,
+                                                                           split_stats=True)
+    out = _ops.qkv_attention(x, stats, wp, colsum, cvec, B, N, H)
+    torch.cuda.synchronize()
+    qkv = _ln64(xq, g64.float().double(), be64.float().double()) @ W64.float().double()
+    if bias:
+        qkv = qkv + b64.float().double()
+    ref = _attn_ref(_q(qkv, "bf16"), B, N, H)   # q / k / v are bf16 operands in both paths
+    torch.testing.assert_close(out.double().cpu(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("B,N,H,D", [(2, 197, 12, 768), (3, 197, 3, 192), (1, 197, 6, 384)])
+def test_qkv_attention_vs_unfused(gpu, B, N, H, D):
+    x, stats, wp, kpad, npad, colsum, cvec, *_ = _case(gpu, B, N, H, D, True, seed=7)
+    out = _ops.qkv_attention(x, stats, wp, colsum, cvec, B, N, H)
+    qkv = _ops.dense("bf16", _lib.EPI_LNIN | _lib.EPI_BIAS, x, wp, kpad, npad, B * N, 3 * H * 64,
+                     bias=cvec, colsum=colsum, stats_in=stats, ln_width=D)
+    ref = _ops.attention("bf16", qkv, B, N, H)
+    torch.cuda.synchronize()
+    d = (out.float() - ref.float()).abs()
+    assert torch.isfinite(out.float()).all()
+    # O is bf16 (2^-9 relative rounding); |O| <~ 3 here
+    assert d.max().item() <= 1.6e-2, d.max().item()
+    assert d.mean().item() <= 1e-3, d.mean().item()
+
+
+def test_qkv_attention_batch_independence(gpu):
+    """Image b's output does not depend on the other images of the batch (bitwise)."""
+    B, N, H, D = 3, 197, 4, 256
+    x, stats, wp, kpad, npad, colsum, cvec, *_ = _case(gpu, B, N, H, D, False, seed=3)
+    out3 = _ops.qkv_attention(x, stats, wp, colsum, cvec, B, N, H)
+    out1 = _ops.qkv_attention(x[N:2 * N].contiguous(), stats[N:2 * N].contiguous(), wp, colsum,
+                              cvec, 1, N, H)
+    torch.cuda.synchronize()
+    assert torch.equal(out3[N:2 * N], out1)
+
+
+def test_qkv_attention_rejects_bad_shapes(gpu):
+    x = torch.zeros((197, 100), dtype=torch.bfloat16, device=gpu)
+    st = torch.zeros((197, 2, 2), device=gpu)
+    w = torch.zeros((256, 128), dtype=torch.bfloat16, device=gpu)
+    v = torch.zeros(256, device=gpu)
+    lib = _lib.load_library()
+    P = lambda t: t.data_ptr()  # noqa: E731
+    o = torch.zeros((197, 64), dtype=torch.bfloat16, device=gpu)
+    # D % 64 != 0, N out of (192, 208]
+    assert lib.evt_qkv_attention(P(x), 100, P(st), P(w), P(v), P(v), 1, 197, 1, 0.125, 1e-5,
+                                 P(o), 64, None) != 0
+    assert lib.evt_qkv_attention(P(x), 64, P(st), P(w), P(v), P(v), 1, 150, 1, 0.125, 1e-5,
+                                 P(o), 64, None) != 0
+
+
+def test_qkv_attention_two_workgroups_per_cu(gpu):
+    """Enough (image, head) items that two workgroups share every CU: the configuration in which
+    a packed-FMA form of the LayerNorm fold went wrong (csrc/qkv_attn.hip qa_fold)."""
+    B, N, H, D = 64, 197, 12, 768
+    x, stats, wp, kpad, npad, colsum, cvec, *_ = _case(gpu, B, N, H, D, True, seed=9)
+    out = _ops.qkv_attention(x, stats, wp, colsum, cvec, B, N, H)
+    qkv = _ops.dense("bf16", _lib.EPI_LNIN | _lib.EPI_BIAS, x, wp, kpad, npad, B * N, 3 * H * 64,
+                     bias=cvec, colsum=colsum, stats_in=stats, ln_width=D)
+    ref = _ops.attention("bf16", qkv, B, N, H)
+    torch.cuda.synchronize()
+    d = (out.float() - ref.float()).abs()
+    assert d.max().item() <= 1.6e-2, d.max().item()
+
+
+def test_model_with_fused_attention_matches_golden(gpu):
+    """DeiT-tiny (N = 197, H = 3) through evt_set_fusion(EVT_FUSE_QKV_ATTENTION) against the
+    reference-pinned golden logits, at the bf16 tolerance of the unfused path."""
+    import os
+
+    import numpy as np
+
+    from edgevisiontransformer_amd.modeling.models.vit import ViT
+    from edgevisiontransformer_amd.weights import make_images, make_vit_params, vit_config
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    z = np.load(os.path.join(repo, "tests", "golden", "deit_tiny_b2.npz"))
+    cfg = vit_config(192, 12, 3, 768)
+    params = make_vit_params(cfg, seed=int(z["param_seed"]))
+    img = make_images(int(z["batch"]), seed=int(z["image_seed"]))
+    lib = _lib.load_library()
+    lib.evt_set_fusion(_lib.FUSE_QKV_ATTENTION)
+    try:
+        m = ViT(dim=192, depth=12, heads=3, mlp_dim=768, dtype="bf16", weights=params, device=gpu)
+        out = m(torch.from_numpy(img).to(gpu)).cpu().numpy().astype(np.float64)
+    finally:
+        lib.evt_set_fusion(0)
+    gold = z["logits"]
+    assert np.abs(out - gold).max() <= 5e-2
+    cos = (out * gold).sum(1) / np.linalg.norm(out, axis=1) / np.linalg.norm(gold, axis=1)
+    assert cos.min() >= 0.999
