@@ -28,6 +28,9 @@ EPI_BIAS, EPI_GELU, EPI_RESID, EPI_POS, EPI_OUT_F32 = 1, 2, 4, 8, 16
 EPI_LNIN, EPI_RESLN, EPI_STATS, EPI_GELU_ERF = 32, 64, 128, 256
 EPI_OUT_MX8 = 512
 FUSE_QKV_ATTENTION = 1  # evt_set_fusion flag (include/evt.h EVT_FUSE_QKV_ATTENTION)
+# evt_model_profile roles (include/evt.h EVT_PROF_*)
+PROF_ROLES = ("patchify", "patch_embed", "qkv", "attention", "out_proj", "fc1", "fc2", "head",
+              "qkv_attention")
 SWIN_MAX_STAGES = 8
 
 
@@ -109,6 +112,8 @@ SIGNATURES = {
     "evt_graph_launch": (_I, [_P, _P]),
     "evt_set_gemm_variant": (_I, [_I]),
     "evt_set_fusion": (_I, [_I]),
+    "evt_model_profile": (_I, [_P, _I]),
+    "evt_model_profile_read": (_I, [_P, _P, _P]),
     "evt_qkv_attention": (_I, [_P, _I, _P, _P, _P, _P, _I, _I, _I, _F, _F, _P, _I64, _P]),
     "evt_pack_weight": (_I, [_I, _P, _P, _I, _I, _P, _I, _I, _P]),
     "evt_ln_fold": (_I, [_I, _P, _I, _I, _P, _P, _P, _I, _I, _P, _P, _P]),

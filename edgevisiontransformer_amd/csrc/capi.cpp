@@ -149,12 +149,43 @@ struct evt_model {
   size_t ws_bytes = 0;
   hipGraph_t graph = nullptr;        // evt_graph_capture
   hipGraphExec_t graph_exec = nullptr;
+  // evt_model_profile: HIP events around every launch of the last forward, by role
+  bool prof = false;
+  std::vector<hipEvent_t> prof_ev;   // pool (pairs)
+  std::vector<int> prof_role;        // role of pair i of the last forward
 };
 
 namespace {
 
 int g_fusion = 0;  // evt_set_fusion (opt-in: the fused kernel is slower today)
 bool fused_attention_enabled() { return (g_fusion & EVT_FUSE_QKV_ATTENTION) != 0; }
+
+// evt_model_profile: a pair of events around each launch of a forward (profiling forwards only)
+struct ProfScope {
+  evt_model* m;
+  hipStream_t s;
+  int pair = -1;
+  ProfScope(evt_model* m_, int role, hipStream_t s_) : m(m_), s(s_) {
+    if (!m->prof) return;
+    pair = (int)m->prof_role.size();
+    while ((int)m->prof_ev.size() < 2 * (pair + 1)) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreate(&e) != hipSuccess) {
+        pair = -1;
+        return;
+      }
+      m->prof_ev.push_back(e);
+    }
+    m->prof_role.push_back(role);
+    (void)hipEventRecord(m->prof_ev[2 * pair], s);
+  }
+  ~ProfScope() {
+    if (pair >= 0) (void)hipEventRecord(m->prof_ev[2 * pair + 1], s);
+  }
+};
+void prof_reset(evt_model* m) {
+  if (m->prof) m->prof_role.clear();
+}
 
 int dev_alloc(evt_model* m, void** p, size_t bytes) {
   if (bytes == 0) bytes = 16;
@@ -419,6 +450,7 @@ int run_encoder(evt_model* m, int B, hipStream_t s) {
                     fused_attention_enabled();
   for (const Layer& L : m->layers) {
     if (fuse) {  // LN1-folded QKV + attention in one kernel (qkv_attn.hip)
+      ProfScope ps(m, EVT_PROF_QKV_ATTENTION, s);
       QkvAttnParams p{};
       p.x = m->x; p.ldx = D; p.stats = m->sx; p.nslots = stats_slots(D);
       p.inv_d = 1.0f / (float)D; p.eps = m->eps;
@@ -428,16 +460,19 @@ int run_encoder(evt_model* m, int B, hipStream_t s) {
       EVT_HIP(qkv_attn_launch(p, s), "qkv_attention");
     } else {
       {  // LN1-folded QKV (attention.py:24)
+        ProfScope ps(m, EVT_PROF_QKV, s);
         DenseCall c;
         c.flags = EPI_LNIN | EPI_BIAS;
         c.A = m->x; c.lda = D; c.C = m->qkv; c.ldc = 3 * L.inner; c.M = rows; c.N = 3 * L.inner;
         c.stats_in = m->sx;
         EVT_RC(dense(m, L.qkv, c, s));
       }
+      ProfScope ps(m, EVT_PROF_ATTENTION, s);
       AttnParams ap{m->qkv, 3 * L.inner, m->o, L.inner, T, L.heads, B, 0.125f * log2e};
       EVT_HIP(attention_launch(m->dtype, ap, s), "attention");
     }
     {  // out-proj + bias + LN1(x) residual -> xm (+ stats); STANDARD: + x
+      ProfScope ps(m, EVT_PROF_OUT_PROJ, s);
       DenseCall c;
       c.flags = m->standard ? (EPI_BIAS | EPI_RESID | EPI_STATS)
                             : (EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS);
@@ -447,6 +482,7 @@ int run_encoder(evt_model* m, int B, hipStream_t s) {
       EVT_RC(dense(m, L.out, c, s));
     }
     {  // LN2-folded FC1 + GELU (ffn.py:8; STANDARD: exact erf GELU)
+      ProfScope ps(m, EVT_PROF_FC1, s);
       DenseCall c;
       c.flags = EPI_LNIN | EPI_BIAS | (m->standard ? EPI_GELU_ERF : EPI_GELU);
       c.A = m->xm; c.lda = D; c.C = m->hbuf; c.ldc = L.ffn_st; c.M = rows; c.N = L.ffn_st;
@@ -454,6 +490,7 @@ int run_encoder(evt_model* m, int B, hipStream_t s) {
       EVT_RC(dense(m, L.fc1, c, s));
     }
     {  // FC2 + bias + LN2(xm) residual -> x (+ stats); STANDARD: + xm
+      ProfScope ps(m, EVT_PROF_FC2, s);
       DenseCall c;
       c.flags = m->standard ? (EPI_BIAS | EPI_RESID | EPI_STATS)
                             : (EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS);
@@ -688,6 +725,7 @@ int evt_model_destroy(evt_model* m) {
   if (!m) return EVT_OK;
   if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
   if (m->graph) (void)hipGraphDestroy(m->graph);
+  for (hipEvent_t e : m->prof_ev) (void)hipEventDestroy(e);
   for (void* p : m->allocs) (void)hipFree(p);
   delete m;
   return EVT_OK;
@@ -775,11 +813,16 @@ int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* 
   const evt_vit_desc& d = m->desc;
   const Shape& sh = m->sh;
   const int D = d.dim, T = sh.T, dt = m->dtype;
+  prof_reset(m);
   // patch embedding (vit.py:45-51): rearrange -> Dense(D) + pos, CLS row = cls + pos[0]
-  EVT_HIP(patchify_launch(dt, img, B, d.in_chans, d.image_size, d.patch_size, m->apatch, m->x,
-                          m->cls, m->pos, D, m->sx, s),
-          "patchify");
   {
+    ProfScope ps(m, EVT_PROF_PATCHIFY, s);
+    EVT_HIP(patchify_launch(dt, img, B, d.in_chans, d.image_size, d.patch_size, m->apatch, m->x,
+                            m->cls, m->pos, D, m->sx, s),
+            "patchify");
+  }
+  {
+    ProfScope ps(m, EVT_PROF_PATCH_EMBED, s);
     DenseCall c;
     c.flags = EPI_BIAS | EPI_POS | EPI_STATS;
     c.A = m->apatch; c.lda = sh.pd; c.C = m->x; c.ldc = D; c.M = B * sh.P; c.N = D;
@@ -787,6 +830,7 @@ int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* 
     EVT_RC(dense(m, m->patch, c, s));
   }
   EVT_RC(m->mx8 ? run_encoder_mx8(m, B, s) : run_encoder(m, B, s));
+  ProfScope ps_head(m, EVT_PROF_HEAD, s);
   if (m->standard) {  // final LayerNorm of the CLS rows folded into the Linear head
     DenseCall c;
     c.flags = EPI_LNIN | EPI_BIAS | EPI_OUT_F32;
@@ -897,6 +941,7 @@ int evt_t2t_forward(evt_model* m, const float* img, int B, float* logits, void* 
   if (B <= 0 || B > m->max_batch)
     return fail(EVT_EINVAL, "batch must be in [1, max_batch=" + std::to_string(m->max_batch) + "]");
   hipStream_t s = (hipStream_t)stream;
+  prof_reset(m);
   const evt_t2t_desc& d = m->tdesc;
   const int dt = d.dtype, D = d.dim, T = m->sh.T, P = m->sh.P, S = d.image_size;
   const int g1 = m->grid[0], g2 = m->grid[1];
@@ -947,6 +992,30 @@ int evt_t2t_forward(evt_model* m, const float* img, int B, float* logits, void* 
     c.A = m->x; c.lda = (int64_t)T * D; c.C = logits; c.ldc = d.num_classes; c.M = B;
     c.N = d.num_classes; c.stats_in = m->sx; c.stats_step = T;
     EVT_RC(dense(m, m->head, c, s));
+  }
+  return EVT_OK;
+}
+
+int evt_model_profile(evt_model* m, int enable) {
+  if (!m) return fail(EVT_EINVAL, "model is NULL");
+  if (m->graph && enable) return fail(EVT_EINVAL, "profiling a model with a captured graph");
+  m->prof = enable != 0;
+  m->prof_role.clear();
+  return EVT_OK;
+}
+
+int evt_model_profile_read(evt_model* m, float* us, int* launches) {
+  if (!m || !us || !launches) return fail(EVT_EINVAL, "null argument");
+  for (int r = 0; r < EVT_PROF_ROLES; ++r) {
+    us[r] = 0.f;
+    launches[r] = 0;
+  }
+  for (size_t i = 0; i < m->prof_role.size(); ++i) {
+    EVT_HIP(hipEventSynchronize(m->prof_ev[2 * i + 1]), "profile sync");
+    float ms = 0.f;
+    EVT_HIP(hipEventElapsedTime(&ms, m->prof_ev[2 * i], m->prof_ev[2 * i + 1]), "profile read");
+    us[m->prof_role[i]] += 1000.f * ms;
+    launches[m->prof_role[i]] += 1;
   }
   return EVT_OK;
 }
@@ -1096,6 +1165,7 @@ int evt_swin_forward(evt_model* m, const float* img, int B, float* logits, void*
   if (B <= 0 || B > m->max_batch)
     return fail(EVT_EINVAL, "batch must be in [1, max_batch=" + std::to_string(m->max_batch) + "]");
   hipStream_t s = (hipStream_t)stream;
+  prof_reset(m);
   const evt_swin_desc& d = m->sdesc;
   const int dt = d.dtype;
   const SwinStage& s0 = m->stages[0];

@@ -128,6 +128,26 @@ int evt_model_destroy(evt_model* model);
  * are diagnostic builds (timeline stamps, main loop only). */
 int evt_set_gemm_variant(int variant);
 
+/* Per-kernel timing of real forwards (the reference times whole models and per-layer micro-models,
+ * tools.py:82-116 / utils.py:322-406; this is the device-side equivalent): while enabled, every
+ * launch of a forward on the model is bracketed by HIP events on its stream, and
+ * evt_model_profile_read returns, per role, the summed device time (us) and launch count of the
+ * LAST forward (it waits for that forward's events). Not for use inside evt_graph_capture. */
+enum {
+  EVT_PROF_PATCHIFY = 0,        /* einops Rearrange (+ CLS row)        vit.py:31-32,45-51 */
+  EVT_PROF_PATCH_EMBED = 1,     /* patch_to_embedding Dense + pos       vit.py:23,46,51 */
+  EVT_PROF_QKV = 2,             /* LN1-folded to_qkv                    attention.py:17,24 */
+  EVT_PROF_ATTENTION = 3,       /* softmax(q k^T) v                     attention.py:20-34 */
+  EVT_PROF_OUT_PROJ = 4,        /* to_out + LN1(x) residual             attention.py:18,35 */
+  EVT_PROF_FC1 = 5,             /* LN2-folded Dense(M, gelu)            ffn.py:8 */
+  EVT_PROF_FC2 = 6,             /* Dense(D) + LN2(xm) residual          ffn.py:9 */
+  EVT_PROF_HEAD = 7,            /* mlp_head / classifier                vit.py:38-39,55 */
+  EVT_PROF_QKV_ATTENTION = 8,   /* fused QKV + attention (evt_set_fusion) */
+  EVT_PROF_ROLES = 9
+};
+int evt_model_profile(evt_model* m, int enable);
+int evt_model_profile_read(evt_model* m, float* us, int* launches);
+
 /* Fused-kernel switches (process-wide; default 0 = the separate QKV GEMM + attention kernels):
  * EVT_FUSE_QKV_ATTENTION runs each bf16 ViT layer's LN1-folded QKV Dense and attention core as
  * one kernel (evt_qkv_attention) where the token count allows. Opt-in: measured slower than the

@@ -1,0 +1,53 @@
+"""evt_model_profile: per-role HIP-event timing of real forwards (the measurement bench.py's
+roofline uses). Launch counts follow the model structure; times are positive and add up to no
+more than the forward's wall time."""
+import time
+
+import pytest
+import torch
+
+from edgevisiontransformer_amd import _lib
+from edgevisiontransformer_amd.profiling import kernel_times
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("fusion", [0, 1])
+def test_profile_roles_deit_tiny(gpu, fusion):
+    from edgevisiontransformer_amd.modeling.models.vit import build_named
+    m = build_named("deit_tiny", dtype="bf16", seed=0, max_batch=8)
+    img = torch.randn((8, 3, 224, 224), device=gpu)
+    logits = torch.empty((8, 1000), device=gpu)
+    lib = _lib.load_library()
+    lib.evt_set_fusion(fusion)
+    try:
+        kt = kernel_times(m, img, logits, forwards=3)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            m.forward_into(img, logits)
+        torch.cuda.synchronize()
+        wall_us = (time.perf_counter() - t0) / 3 * 1e6
+    finally:
+        lib.evt_set_fusion(0)
+    expect = {"patchify": 1, "patch_embed": 1, "out_proj": 12, "fc1": 12, "fc2": 12, "head": 1}
+    if fusion:
+        expect["qkv_attention"] = 12
+    else:
+        expect.update(qkv=12, attention=12)
+    assert {k: v["launches"] for k, v in kt.items()} == expect
+    assert all(v["us_per_launch"] > 0 for v in kt.values())
+    total = sum(v["us_per_launch"] * v["launches"] for v in kt.values())
+    assert total <= 1.2 * wall_us, (total, wall_us)
+
+
+def test_profile_off_leaves_forward_unchanged(gpu):
+    from edgevisiontransformer_amd.modeling.models.vit import build_named
+    m = build_named("deit_tiny", dtype="bf16", seed=0, max_batch=2)
+    img = torch.randn((2, 3, 224, 224), device=gpu)
+    a, b = torch.empty((2, 1000), device=gpu), torch.empty((2, 1000), device=gpu)
+    m.forward_into(img, a)
+    kernel_times(m, img, b, forwards=1)
+    m.forward_into(img, b)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
