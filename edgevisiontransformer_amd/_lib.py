@@ -121,6 +121,7 @@ SIGNATURES = {
     "evt_attention": (_I, [_I, _P, _I64, _P, _I64, _I, _I, _I, _F, _P]),
     "evt_layernorm": (_I, [_I, _P, _I64, _P, _I64, _P, _P, _I, _I, _F, _P]),
     "evt_patchify": (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P]),
+    "evt_patchify_cm": (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P]),
     "evt_t2t_num_weights": (_I, [ctypes.POINTER(evt_t2t_desc)]),
     "evt_t2t_create": (_I, [ctypes.POINTER(evt_t2t_desc), ctypes.POINTER(_P), _I, _P,
                             ctypes.POINTER(_P)]),

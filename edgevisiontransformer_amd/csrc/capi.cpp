@@ -105,6 +105,7 @@ struct evt_model {
   int family = 0;            // 0: ViT / ViT_Pruned, 1: T2T-ViT, 2: Swin
   bool standard = false;     // ViT with EVT_VIT_STANDARD semantics
   bool mx8 = false;          // EVT_DTYPE_MX8: MXFP8 encoder Dense layers (dtype is then bf16)
+  bool patch_cm = false;     // ViT: channel-major patch vectors / patch weight rows
   void* qa = nullptr;        // MX8: [rows][max(Dpad, innerpad)] e4m3 A operand (LN out / attn out)
   uint32_t* sa = nullptr;    // MX8: its scales [pad/128][rows]
   void* qh = nullptr;        // MX8: [rows][ffnpad] FC1 output (e4m3, zero-initialised)
@@ -761,7 +762,15 @@ int evt_vit_create(const evt_vit_desc* desc, const float* const* w, int n_weight
   m->sh = sh;
   const int D = desc->dim;
   auto run = [&]() -> int {
-    EVT_RC(make_dense(m, &m->patch, w[0], w[1], sh.pd, D, s));
+    if (desc->patch_size % 8 == 0) {  // channel-major patch vectors (patchify_cm_kernel)
+      float* wcm = nullptr;
+      EVT_RC(dev_alloc(m, (void**)&wcm, (size_t)sh.pd * D * sizeof(float)));
+      EVT_HIP(patch_weight_cm(w[0], wcm, desc->in_chans, desc->patch_size, D, s), "patch weight");
+      EVT_RC(make_dense(m, &m->patch, wcm, w[1], sh.pd, D, s));
+      m->patch_cm = true;
+    } else {
+      EVT_RC(make_dense(m, &m->patch, w[0], w[1], sh.pd, D, s));
+    }
     EVT_RC(copy_vec(m, &m->cls, w[2], D, s));
     EVT_RC(copy_vec(m, &m->pos, w[3], (size_t)sh.T * D, s));
     EVT_RC(build_encoder(m, w + 4, s));
@@ -818,7 +827,7 @@ int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* 
   {
     ProfScope ps(m, EVT_PROF_PATCHIFY, s);
     EVT_HIP(patchify_launch(dt, img, B, d.in_chans, d.image_size, d.patch_size, m->apatch, m->x,
-                            m->cls, m->pos, D, m->sx, s),
+                            m->cls, m->pos, D, m->sx, s, m->patch_cm),
             "patchify");
   }
   {
@@ -1489,6 +1498,16 @@ int evt_patchify(int dtype, const float* img, int B, int C, int HW, int ps, void
   EVT_HIP(patchify_launch(dtype, img, B, C, HW, ps, out, x, cls, pos, D, stats,
                           (hipStream_t)stream),
           "patchify");
+  return EVT_OK;
+}
+
+int evt_patchify_cm(int dtype, const float* img, int B, int C, int HW, int ps, void* out, void* x,
+                    const float* cls, const float* pos, int D, float* stats, void* stream) {
+  if (!img || !out || !x || !cls || !pos || B < 0 || C <= 0 || ps <= 0 || HW % ps || ps % 8)
+    return fail(EVT_EINVAL, "patchify_cm: bad shape (ps % 8 == 0)");
+  EVT_HIP(patchify_launch(dtype, img, B, C, HW, ps, out, x, cls, pos, D, stats,
+                          (hipStream_t)stream, true),
+          "patchify_cm");
   return EVT_OK;
 }
 

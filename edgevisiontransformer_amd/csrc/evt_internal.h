@@ -116,9 +116,13 @@ __host__ __device__ inline int stats_slots(int D) { return 2 * ((D + 255) / 256)
 // NCHW fp32 images -> patch matrix [B*P, p*p*C] (p1 p2 c) in activation dtype; also writes
 // the CLS token row x[b*(P+1)] = cls + pos[0] (activation dtype, row stride D) and, when stats is
 // non-null, its (sum, sumsq) into slot 0 of stats[b*(P+1)] (other slots zeroed).
+// channel_major: the patch vector's K axis in (c p1 p2) order instead (the model's layout; the
+// patch weight then packed from patch_weight_cm's row permutation); requires ps % 8 == 0.
 hipError_t patchify_launch(int dtype, const float* img, int B, int C, int HW, int ps, void* out,
                            void* x, const float* cls, const float* pos, int D, float* stats,
-                           hipStream_t s);
+                           hipStream_t s, bool channel_major = false);
+// Keras patch_to_embedding kernel W [(p1 p2 c), N] -> Wcm [(c p1 p2), N] (rows permuted).
+hipError_t patch_weight_cm(const float* W, float* Wcm, int C, int ps, int N, hipStream_t s);
 
 // ---- T2T stage (t2t.hip) ----
 struct PerformerWeights {  // fp32 device pointers, Keras layouts

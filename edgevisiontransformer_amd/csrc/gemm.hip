@@ -1557,6 +1557,8 @@ hipError_t launch_big(const GemmParams& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_big_kernel<FL, 6, true>), grid, dim3(512), 0, s, q);
   else if (g_gemm_variant == 108)
     hipLaunchKernelGGL((gemm_big_kernel<FL, 8, true>), grid, dim3(512), 0, s, q);
+  else if constexpr ((FL & EPI_POS) != 0)  // patch embedding: 8-phase loop (153 vs 179 us, bs512)
+    hipLaunchKernelGGL((gemm_big_kernel<FL, 8>), grid, dim3(512), 0, s, q);
   else
     hipLaunchKernelGGL((gemm_big_kernel<FL, 6>), grid, dim3(512), 0, s, q);
   return hipGetLastError();

@@ -123,6 +123,72 @@ __global__ __launch_bounds__(256) void patchify_kernel(const float* __restrict__
   }
 }
 
+// Channel-major patch vectors (the model's layout): out[patch][c ps ps + p1 ps + p2], i.e. the
+// reference vector (p1 p2 c) with its K axis permuted; the patch-embedding weight is packed with
+// the same row permutation (patch_weight_cm), so the product is the reference Dense. Each patch
+// vector is then C * ps runs of ps contiguous image pixels: every thread reads 8 consecutive
+// pixels of one run from the LDS strip (two 16-B reads) and writes one 16-B (bf16) chunk, and a
+// wave's stores cover 1 KB of consecutive output. grid (HW/ps, B); requires ps % 8 == 0.
+template <typename TO>
+__global__ __launch_bounds__(256) void patchify_cm_kernel(const float* __restrict__ img, int C,
+                                                          int HW, int ps, TO* __restrict__ out,
+                                                          TO* __restrict__ x,
+                                                          const float* __restrict__ cls,
+                                                          const float* __restrict__ pos, int D,
+                                                          float* __restrict__ stats) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* strip = (float*)smem;
+  const int hh = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int np = HW / ps;
+  const int per_c = ps * HW;
+  for (int c = 0; c < C; ++c) {
+    const float* src = img + (((int64_t)b * C + c) * HW + (int64_t)hh * ps) * HW;
+    for (int i = tid * 4; i < per_c; i += 256 * 4) *(f32x4*)(strip + c * per_c + i) = load4(src + i);
+  }
+  __syncthreads();
+  const int pd = ps * ps * C;
+  const int cpr = ps / 8;        // 8-pixel chunks per run
+  const int cpp = pd / 8;        // chunks per patch vector
+  TO* orow = out + ((int64_t)b * np * np + (int64_t)hh * np) * pd;
+  for (int e = tid; e < np * cpp; e += 256) {
+    const int ww = e / cpp, q = e - ww * cpp;
+    const int run = q / cpr, c = run / ps, p1 = run - c * ps, p2 = (q - run * cpr) * 8;
+    const float* sp = strip + c * per_c + p1 * HW + ww * ps + p2;
+    const f32x4 v0 = *(const f32x4*)sp, v1 = *(const f32x4*)(sp + 4);
+    TO* op = orow + (int64_t)ww * pd + q * 8;
+    store4(op, v0);
+    store4(op + 4, v1);
+  }
+  if (hh == 0 && tid < 64) {  // one wave writes the CLS row and its LayerNorm statistics
+    const int64_t row = (int64_t)b * (np * np + 1);
+    TO* xr = x + row * D;
+    float s1 = 0.f, s2 = 0.f;
+    for (int n = tid; n < D; n += 64) {
+      const TO v = from_f32<TO>(cls[n] + pos[n]);
+      xr[n] = v;
+      const float q = to_f32(v);
+      s1 += q;
+      s2 += q * q;
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (stats && tid < stats_slots(D)) {
+      float* st = stats + 2 * (stats_slots(D) * row + tid);
+      st[0] = tid == 0 ? s1 : 0.f;
+      st[1] = tid == 0 ? s2 : 0.f;
+    }
+  }
+}
+
+// Keras patch_to_embedding kernel [(p1 p2 c), N] -> rows in the channel-major order above.
+__global__ void patch_weight_cm_kernel(const float* __restrict__ W, float* __restrict__ Wcm, int C,
+                                       int ps, int N) {
+  const int kcm = blockIdx.x;  // c ps ps + p1 ps + p2
+  const int c = kcm / (ps * ps), p12 = kcm - c * ps * ps;
+  const int k = p12 * C + c;   // (p1 ps + p2) C + c
+  for (int n = threadIdx.x; n < N; n += blockDim.x) Wcm[(int64_t)kcm * N + n] = W[(int64_t)k * N + n];
+}
+
 template <typename TO, int NV>
 hipError_t ln_nv(const float* x, int64_t ldx, void* y, int64_t ldy, const float* g,
                  const float* bb, int rows, int D, float eps, hipStream_t s) {
@@ -151,14 +217,34 @@ hipError_t layernorm_launch(int dtype, const float* x, int64_t ldx, void* y, int
                           : ln_t<float>(x, ldx, y, ldy, gamma, beta, rows, D, eps, s);
 }
 
+hipError_t patch_weight_cm(const float* W, float* Wcm, int C, int ps, int N, hipStream_t s) {
+  hipLaunchKernelGGL(patch_weight_cm_kernel, dim3(C * ps * ps), dim3(256), 0, s, W, Wcm, C, ps, N);
+  return hipGetLastError();
+}
+
 hipError_t patchify_launch(int dtype, const float* img, int B, int C, int HW, int ps, void* out,
                            void* x, const float* cls, const float* pos, int D, float* stats,
-                           hipStream_t s) {
+                           hipStream_t s, bool channel_major) {
   if (B <= 0) return hipSuccess;
   if (HW % ps || (ps * HW) % 4) return hipErrorInvalidValue;
   const size_t lds = (size_t)C * ps * HW * sizeof(float);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   dim3 grid(HW / ps, B);
+  if (channel_major) {
+    if (ps % 8) return hipErrorInvalidValue;
+    if (dtype == DT_BF16) {
+      hipFuncSetAttribute((const void*)patchify_cm_kernel<bf16>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(patchify_cm_kernel<bf16>, grid, dim3(256), lds, s, img, C, HW, ps,
+                         (bf16*)out, (bf16*)x, cls, pos, D, stats);
+    } else {
+      hipFuncSetAttribute((const void*)patchify_cm_kernel<float>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(patchify_cm_kernel<float>, grid, dim3(256), lds, s, img, C, HW, ps,
+                         (float*)out, (float*)x, cls, pos, D, stats);
+    }
+    return hipGetLastError();
+  }
   if (dtype == DT_BF16) {
     hipFuncSetAttribute((const void*)patchify_kernel<bf16>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -233,6 +233,13 @@ int evt_layernorm(int dtype, const float* x, int64_t ldx, void* y, int64_t ldy,
 int evt_patchify(int dtype, const float* img, int B, int C, int HW, int ps, void* out, void* x,
                  const float* cls, const float* pos, int D, float* stats, void* stream);
 
+/* evt_patchify with the patch vector's K axis in channel-major (c p1 p2) order - the layout the
+ * model uses: each vector is C*ps runs of ps contiguous pixels (a streaming gather), and the
+ * model packs its patch-embedding weight rows in the same permuted order, so the product is the
+ * reference Dense of the (p1 p2 c) vector. ps % 8 == 0. */
+int evt_patchify_cm(int dtype, const float* img, int B, int C, int HW, int ps, void* out, void* x,
+                    const float* cls, const float* pos, int D, float* stats, void* stream);
+
 /* ---- T2T-ViT (reference modeling/models/t2t_vit.py) ------------------------------------ */
 
 /* Static shape of a T2T_ViT (t2t_vit.py:91-114; factories get_t2t_vit_{7,10,12,14} :138-148).

@@ -81,14 +81,17 @@ def layernorm(dtype, x, gamma, beta, eps=1e-5):
     return y
 
 
-def patchify(dtype, img, ps, cls, pos, D):
+def patchify(dtype, img, ps, cls, pos, D, channel_major=False):
+    """evt_patchify ((p1 p2 c) vectors) or, channel_major, evt_patchify_cm ((c p1 p2))."""
     B, C, HW, _ = img.shape
     P = (HW // ps) ** 2
     out = torch.empty((B * P, ps * ps * C), dtype=TDT[dtype], device=img.device)
     x = torch.zeros((B * (P + 1), D), dtype=TDT[dtype], device=img.device)
     stats = torch.full((B * (P + 1), 2 * ((D + 255) // 256), 2), -1.0, device=img.device)
-    _lib.check(_lib.load_library().evt_patchify(_lib.DTYPE[dtype], _p(img), B, C, HW, ps, _p(out),
-                                                _p(x), _p(cls), _p(pos), D, _p(stats), _s()))
+    lib = _lib.load_library()
+    fn = lib.evt_patchify_cm if channel_major else lib.evt_patchify
+    _lib.check(fn(_lib.DTYPE[dtype], _p(img), B, C, HW, ps, _p(out), _p(x), _p(cls), _p(pos), D,
+                  _p(stats), _s()))
     return out, x, stats
 
 

@@ -149,13 +149,19 @@ def test_layernorm(gpu, dtype, rows, D):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f32"])
-def test_patchify(gpu, dtype):
+@pytest.mark.parametrize("channel_major", [False, True])
+def test_patchify(gpu, dtype, channel_major):
+    """evt_patchify: the reference (p1 p2 c) vectors; evt_patchify_cm (the model's layout): the
+    same vectors with K permuted to (c p1 p2), bit-exact either way."""
     B, C, HW, ps, D = 2, 3, 224, 16, 192
     img = _rand((B, C, HW, HW), 31).float()
     cls, pos = _rand((D,), 32).float(), _rand((197, D), 33).float()
-    out, x, stats = _ops.patchify(dtype, img.to(gpu), ps, cls.to(gpu), pos.to(gpu), D)
+    out, x, stats = _ops.patchify(dtype, img.to(gpu), ps, cls.to(gpu), pos.to(gpu), D,
+                                  channel_major=channel_major)
     torch.cuda.synchronize()
     ref = vit_ref.patchify_nchw(img.numpy(), ps).reshape(B * 196, -1)
+    if channel_major:  # (p1 p2 c) -> (c p1 p2)
+        ref = ref.reshape(B * 196, ps, ps, C).transpose(0, 3, 1, 2).reshape(B * 196, -1)
     exp = torch.from_numpy(ref).to(_ops.TDT[dtype])
     assert torch.equal(out.cpu(), exp), "patchify is a pure permutation: must be bit-exact"
     xr = x.cpu().reshape(B, 197, D)

@@ -1,6 +1,6 @@
 """evt_model_profile: per-role HIP-event timing of real forwards (the measurement bench.py's
 roofline uses). Launch counts follow the model structure; times are positive and add up to no
-more than the forward's wall time."""
+more than the wall time of the profiled forwards."""
 import time
 
 import pytest
@@ -21,13 +21,11 @@ def test_profile_roles_deit_tiny(gpu, fusion):
     lib = _lib.load_library()
     lib.evt_set_fusion(fusion)
     try:
-        kt = kernel_times(m, img, logits, forwards=3)
+        kernel_times(m, img, logits, forwards=1)  # warm-up (event pool)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(3):
-            m.forward_into(img, logits)
-        torch.cuda.synchronize()
-        wall_us = (time.perf_counter() - t0) / 3 * 1e6
+        kt = kernel_times(m, img, logits, forwards=3)
+        wall_us = (time.perf_counter() - t0) / 3 * 1e6  # per profiled forward (+ one extra)
     finally:
         lib.evt_set_fusion(0)
     expect = {"patchify": 1, "patch_embed": 1, "out_proj": 12, "fc1": 12, "fc2": 12, "head": 1}
@@ -37,8 +35,9 @@ def test_profile_roles_deit_tiny(gpu, fusion):
         expect.update(qkv=12, attention=12)
     assert {k: v["launches"] for k, v in kt.items()} == expect
     assert all(v["us_per_launch"] > 0 for v in kt.values())
+    # the bracketed intervals are disjoint and in stream order: their sum fits in the wall time
     total = sum(v["us_per_launch"] * v["launches"] for v in kt.values())
-    assert total <= 1.2 * wall_us, (total, wall_us)
+    assert total <= wall_us, (total, wall_us)
 
 
 def test_profile_off_leaves_forward_unchanged(gpu):
