@@ -183,13 +183,32 @@ __device__ __forceinline__ void attn_tile_bf16(const AttnParams& p, const EVT_LD
     }
     return;
   }
-  if (q < p.N) {
-    const float inv = 1.0f / sum;
-    bf16* op = (bf16*)p.out + ((int64_t)b * p.N + q) * p.ldo + h * 64 + 4 * g;
+  // bf16 pairs, then one permlane16 swap per dword of each (dt, dt + 1) pair: lane group g ends
+  // up with features 32 pr + 16 (g & 1) + 8 (g >> 1) .. + 7 of its query in {x[0..1], y[0..1]},
+  // so O leaves as two 16-B stores per lane instead of four 8-B ones (store-issue bound)
+  const float inv = 1.0f / sum;
+  u32x2 ob[4];
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      if (PLAIN_STORE) store4(op + dt * 16, o[dt] * inv);
-      else store4_nt(op + dt * 16, o[dt] * inv);
+  for (int dt = 0; dt < 4; ++dt) {
+    const f32x4 v = o[dt] * inv;
+    const bf16x4 w = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+    ob[dt] = __builtin_bit_cast(u32x2, w);
+  }
+  unsigned x0[2], x1[2], y0[2], y1[2];
+#pragma unroll
+  for (int pr = 0; pr < 2; ++pr) {
+    unsigned a0 = ob[2 * pr][0], a1 = ob[2 * pr][1], c0 = ob[2 * pr + 1][0], c1 = ob[2 * pr + 1][1];
+    permlane16_swap(a0, c0);
+    permlane16_swap(a1, c1);
+    x0[pr] = a0; x1[pr] = a1; y0[pr] = c0; y1[pr] = c1;
+  }
+  if (q < p.N) {
+    bf16* op = (bf16*)p.out + ((int64_t)b * p.N + q) * p.ldo + h * 64 + 16 * (g & 1) + 8 * (g >> 1);
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const u32x4 v = {x0[pr], x1[pr], y0[pr], y1[pr]};
+      if (PLAIN_STORE) *(u32x4*)(op + 32 * pr) = v;
+      else __builtin_nontemporal_store(v, (u32x4*)(op + 32 * pr));
     }
   }
 }

@@ -1458,8 +1458,11 @@ int evt_dense(int dtype, const evt_dense_args* a, void* stream) {
 
 int evt_attention(int dtype, const void* qkv, int64_t ldq, void* out, int64_t ldo, int B, int N,
                   int H, float scale, void* stream) {
-  if (!qkv || !out || B < 0 || N <= 0 || N > 256 || H <= 0 || ldq < 3 * H * 64 || ldo < H * 64)
-    return fail(EVT_EINVAL, "attention: bad shape (N <= 256, head size 64)");
+  // 16-B Q / O accesses: row pitches of 16 bytes multiple, 16-B aligned bases
+  const int64_t vec = dtype == DT_BF16 ? 8 : 4;
+  if (!qkv || !out || B < 0 || N <= 0 || N > 256 || H <= 0 || ldq < 3 * H * 64 || ldo < H * 64 ||
+      ldq % vec || ldo % vec || (((uintptr_t)qkv | (uintptr_t)out) & 15))
+    return fail(EVT_EINVAL, "attention: bad shape (N <= 256, head size 64, 16-B aligned rows)");
   AttnParams p{qkv, ldq, out, ldo, N, H, B, scale * 1.4426950408889634f};
   EVT_HIP(attention_launch(dtype, p, (hipStream_t)stream), "attention");
   return EVT_OK;

@@ -38,6 +38,15 @@ __device__ __forceinline__ void store4(bf16* p, f32x4 v) {
   *(bf16x4*)p = o;
 }
 
+// v_permlane16_swap_b32 on two dwords: odd 16-lane rows of x <-> even rows of y (lanes 16-31 of x
+// with lanes 0-15 of y, 48-63 of x with 32-47 of y). Scalars only: applied to vector elements in a
+// loop, hipcc 7.2 miscompiles the builtin (it reuses element 0 for every j).
+__device__ __forceinline__ void permlane16_swap(unsigned& x, unsigned& y) {
+  const auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+  x = (unsigned)r[0];
+  y = (unsigned)r[1];
+}
+
 // Non-temporal (streaming) stores for GEMM outputs: they go to HBM without displacing the operand
 // panels the other CUs of the XCD still read from L2 (measured: -15% on the K = 768 GEMMs).
 __device__ __forceinline__ void store4_nt(float* p, f32x4 v) { __builtin_nontemporal_store(v, (f32x4*)p); }
