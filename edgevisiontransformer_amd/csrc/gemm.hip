@@ -1125,7 +1125,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* mat, int
 template <int FL, int DBG = 0, bool PADN = true>
 __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
                                               int wave, int wm, int wn, int m0, int n0, int tn,
-                                              int lane, bool interior) {
+                                              int lane, bool interior, int iter = 0) {
+  // DBG 3: sub-stamps 3..5 of the tile's timeline row (wave 0, lane 0)
+  auto stamp = [&](int k) {
+    if (DBG == 3 && wave == 0 && lane == 0 && iter < 16)
+      ((unsigned long long*)p.pos)[((int64_t)blockIdx.x * 16 + iter) * 8 + k] = __builtin_amdgcn_s_memtime();
+  };
   asm volatile("" : "+v"(lane));  // keep lane-derived addresses out of the persistent loop (VGPRs)
   if constexpr (DBG == 2) {  // ablation: no epilogue at all, accumulators kept live by a dead store
     float sink = 0.f;
@@ -1192,6 +1197,7 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
       for (int mt = 0; mt < 8; ++mt) acc[nt][mt] = gelu4(acc[nt][mt], (FL & EPI_GELU) ? 0 : 2);
     }
   }
+  stamp(3);
   // 2. store layout: pair (2k, 2k+1) -> lane row wm*128 + (2k + (fg & 1))*16 + frow, columns
   //    wn*64 + nt*16 + (fg >> 1)*8 + [acc[nt][2k][0..3], acc[nt][2k+1][0..3]]
 #pragma unroll
@@ -1206,7 +1212,12 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
   // 3. residual (16-B buffer loads in the store layout, all issued up front), bf16 stores and the
   //    row statistics of the stored values; nt-major so each column-vector slice is read once
   u32x4 rr[4][4];
-  if constexpr ((FL & EPI_RESID) != 0) {
+  if constexpr (DBG == 7) {  // ablation: no residual loads (zeros)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) rr[k][nt] = u32x4{0u, 0u, 0u, 0u};
+  } else if constexpr ((FL & EPI_RESID) != 0) {
     const __amdgpu_buffer_rsrc_t rs = tile_rsrc(p.resid, p.ldr, p.M, m0, n0);
     const int vo = (rl * (int)p.ldr + cl) * 2;
 #pragma unroll
@@ -1272,6 +1283,7 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
       }
     }
   }
+  stamp(4);
   // 4. output: per row pair k, the wave's 32 x 64 block goes through its private 4 KiB of LDS
   //    (free during the epilogue: buffer-1 regions 2 / 3 are only DMA'd in the next tile's
   //    phases 1 / 2) and leaves as whole 128-B row segments, 8 rows per store instruction
@@ -1307,6 +1319,7 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
   }
+  stamp(5);
   if constexpr ((FL & EPI_STATS) != 0) {
     // lanes fg and fg ^ 2 hold the two 32-column halves of the same row
 #pragma unroll
@@ -1354,7 +1367,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
   int iter = 0;
   auto stamp = [&](int k) {  // DBG 3: timeline of block's tiles (s_memtime, wave 0)
     if ((DBG == 3 || DBG == 5) && tid == 0 && iter < 16)
-      ((unsigned long long*)p.pos)[((int64_t)blockIdx.x * 16 + iter) * 4 + k] = __builtin_amdgcn_s_memtime();
+      ((unsigned long long*)p.pos)[((int64_t)blockIdx.x * 16 + iter) * 8 + k] = __builtin_amdgcn_s_memtime();
   };
   while (true) {
     const int m0 = tm * BIG_BM, n0 = tn * BIG_BN;
@@ -1387,8 +1400,8 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
     if constexpr (DBG == 6)  // A/B: the round-1 epilogue
       pers_epilogue_v1<FL, 0, PADN>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior);
     else
-      pers_epilogue<FL, DBG, PADN>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior);
-    stamp(3);
+      pers_epilogue<FL, DBG, PADN>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior, iter);
+    stamp(7);
     ++iter;
     if (!has_next) break;
     if (!interior || DBG == 1 || DBG == 2) wait_vmcnt0();
@@ -1586,7 +1599,7 @@ constexpr bool pers_fl(int fl) {
 
 // persistent kernel: supported epilogue, 8-column output groups, LN rows of <= 8 slots
 bool use_pers(const GemmParams& p, int flags) {
-  if (g_gemm_variant != 0 && (g_gemm_variant < 9 || g_gemm_variant > 19 || g_gemm_variant == 12 ||
+  if (g_gemm_variant != 0 && (g_gemm_variant < 9 || g_gemm_variant > 20 || g_gemm_variant == 12 ||
                               g_gemm_variant == 14))
     return false;
   if (p.N % 8 || p.vec_ok < 2) return false;
@@ -1613,6 +1626,8 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 6, false>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 17)  // ablation: main loop + tile loop only (no epilogue)
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 2, false>), dim3(G), dim3(512), 0, s, q, total);
+  else if (g_gemm_variant == 20)  // ablation: no residual loads (out-proj 153 -> 115 us)
+    hipLaunchKernelGGL((gemm_pers_kernel<FL, 7, false>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 18)  // ablation: epilogue without the GELU
     hipLaunchKernelGGL((gemm_pers_kernel<(FL & ~(EPI_GELU | EPI_GELU_ERF)), 0, false>), dim3(G),
                        dim3(512), 0, s, q, total);

@@ -55,7 +55,7 @@ for name, (K, N, fl) in shapes.items():
         outs[v] = torch.empty((M, N + LDC_PAD), dtype=torch.float32 if fl & 16 else torch.bfloat16,
                               device="cuda")
     def run(v):
-        lib.evt_set_gemm_variant(v)
+        _lib.check(lib.evt_set_gemm_variant(v))
         a = _lib.evt_dense_args()
         a.flags, a.A, a.lda, a.Wp, a.Kpad, a.Npad = fl, A.data_ptr(), K, wp.data_ptr(), K, npad
         a.C, a.ldc, a.M, a.N, a.bias = outs[v].data_ptr(), N + LDC_PAD, M, N, bias.data_ptr()

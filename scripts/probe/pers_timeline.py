@@ -39,7 +39,7 @@ for spec in os.environ.get("GS", "768x3072@35,768x2304@33,768x768@197,3072x768@1
     rg, rb = torch.ones(N, device="cuda"), torch.zeros(N, device="cuda")
     sto = torch.zeros((M, nso, 2), device="cuda")
     C = torch.empty((M, N), dtype=torch.bfloat16, device="cuda")
-    dbg = torch.zeros(256 * 16 * 4, dtype=torch.int64, device="cuda")
+    dbg = torch.zeros(256 * 16 * 8, dtype=torch.int64, device="cuda")
     a = _lib.evt_dense_args()
     a.flags, a.A, a.lda, a.Wp, a.Kpad, a.Npad = fl, A.data_ptr(), K, wp.data_ptr(), K, npad
     a.C, a.ldc, a.M, a.N, a.bias = C.data_ptr(), N, M, N, bias.data_ptr()
@@ -53,15 +53,17 @@ for spec in os.environ.get("GS", "768x3072@35,768x2304@33,768x768@197,3072x768@1
     if fl & 32:
         a.colsum, a.stats_in, a.ln_width, a.ln_eps = colsum.data_ptr(), stats.data_ptr(), K, 1e-5
     for v in (9, TV, TV):
-        lib.evt_set_gemm_variant(v)
+        _lib.check(lib.evt_set_gemm_variant(v))
         _lib.check(lib.evt_dense(1, ctypes.byref(a), S()))
         torch.cuda.synchronize()
     lib.evt_set_gemm_variant(0)
-    t = dbg.cpu().numpy().reshape(256, 16, 4).astype(np.float64)
+    t = dbg.cpu().numpy().reshape(256, 16, 8).astype(np.float64)
     valid = t[:, :, 0] > 0
     seg = {"main": t[:, :, 1] - t[:, :, 0], "coef+issue": t[:, :, 2] - t[:, :, 1],
-           "epilogue": t[:, :, 3] - t[:, :, 2]}
-    nxt = t[:, 1:, 0] - t[:, :-1, 3]
+           "epi:fold/gelu": t[:, :, 3] - t[:, :, 2], "epi:swap/resid/stats": t[:, :, 4] - t[:, :, 3],
+           "epi:stores": t[:, :, 5] - t[:, :, 4], "epi:statx": t[:, :, 7] - t[:, :, 5],
+           "epilogue": t[:, :, 7] - t[:, :, 2]}
+    nxt = t[:, 1:, 0] - t[:, :-1, 7]
     out = {k: (np.median(v[valid]), np.percentile(v[valid], 90)) for k, v in seg.items()}
     out["gap"] = (np.median(nxt[valid[:, 1:]]), 0)
     # per-iteration medians of main loop (first tiles are special)
