@@ -140,6 +140,7 @@ struct evt_model {
   void* qkv = nullptr;       // [B*T, 3*inner]
   void* o = nullptr;         // [B*T, inner]
   void* hbuf = nullptr;      // [B*T, ffn_st]
+  size_t hbuf_bytes = 0;
   void* hh = nullptr;        // [B, head_st]
   void* sk = nullptr;        // stream-K scratch of the model's GEMMs (gemm_sk_bytes)
   // Swin (family 2)
@@ -440,6 +441,24 @@ int alloc_encoder_ws(evt_model* m, int B, size_t hbuf_bytes, hipStream_t s) {
   EVT_RC(dev_alloc(m, &m->qkv, rows * 3 * m->sh.max_inner * es));
   EVT_RC(dev_alloc(m, &m->o, rows * m->sh.max_inner * es));
   EVT_RC(dev_alloc(m, &m->hbuf, hbuf_bytes));
+  m->hbuf_bytes = hbuf_bytes;
+  return EVT_OK;
+}
+
+// Small-M, long-K Dense layers (the classifier head: M = batch) as K splits in one launch when the
+// plain tile grid would leave most CUs idle; fp32 partials in the (then idle) hidden buffer.
+int dense_head(const evt_model* m, const DenseW& w, const DenseCall& c, hipStream_t s) {
+  const int tiles = ((c.M + GEMM_BM - 1) / GEMM_BM) * (w.npad / GEMM_BN);
+  int S = 1;
+  while (S < 8 && tiles * S * 2 <= 256 && w.kpad % (S * 2 * PAD_K) == 0) S *= 2;
+  const size_t part = (size_t)S * c.M * w.npad * sizeof(float);
+  if (S < 2 || !m->hbuf || part > m->hbuf_bytes ||
+      (c.flags & ~(EPI_BIAS | EPI_GELU | EPI_OUT_F32)))
+    return dense(m, w, c, s);
+  GemmParams p{};
+  p.A = c.A; p.lda = c.lda; p.W = w.w; p.ldw = w.kpad; p.C = c.C; p.ldc = c.ldc;
+  p.M = c.M; p.N = c.N; p.K = w.kpad; p.ntiles = w.npad / GEMM_BN; p.bias = w.b;
+  EVT_HIP(gemm_splitk_launch(m->dtype, c.flags, p, S, (float*)m->hbuf, s), "dense (split-K)");
   return EVT_OK;
 }
 
@@ -853,14 +872,14 @@ int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* 
     DenseCall c;
     c.flags = EPI_BIAS | EPI_GELU;
     c.A = m->x; c.lda = (int64_t)T * D; c.C = m->hh; c.ldc = sh.head_st; c.M = B; c.N = sh.head_st;
-    EVT_RC(dense(m, m->head1, c, s));
+    EVT_RC(dense_head(m, m->head1, c, s));
   }
   {
     DenseCall c;
     c.flags = EPI_BIAS | EPI_OUT_F32;
     c.A = m->hh; c.lda = sh.head_st; c.C = logits; c.ldc = d.num_classes; c.M = B;
     c.N = d.num_classes;
-    EVT_RC(dense(m, m->head2, c, s));
+    EVT_RC(dense_head(m, m->head2, c, s));
   }
   return EVT_OK;
 }

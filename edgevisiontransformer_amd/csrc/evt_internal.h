@@ -48,6 +48,8 @@ struct GemmParams {
   int stats_step;                     // EPI_LNIN: A row m reads stats_in row m * stats_step (0 = 1)
   int* sk_flags;                      // stream-K hand-off flags [>= #CUs] (zero between launches)
   float* sk_part;                     // stream-K partial tiles [#CUs][256 * 256] fp32
+  int ks_chunk;                       // split-K (128x128 kernel, gridDim.y splits): K per split;
+  int64_t ks_stride;                  // fp32 partial C of split z at C + z * ks_stride
 };
 constexpr int GEMM_BM = 128;
 constexpr int GEMM_BN = 128;
@@ -56,6 +58,11 @@ constexpr int PAD_K = 64;   // K granularity (elements) of every packed operand
 constexpr int PAD_N = 64;   // column granularity of activation buffers
 
 hipError_t gemm_launch(int dtype, int flags, const GemmParams& p, hipStream_t s);
+// Skinny GEMM (small M, long K: the classifier head) as S K-splits in one launch, fp32 partials
+// part[S][M][ntiles*128], then a fixed-order reduction + bias (+ GELU) into C (deterministic).
+// flags: EPI_BIAS and/or EPI_GELU and/or EPI_OUT_F32 only; K % (S * 64) == 0.
+hipError_t gemm_splitk_launch(int dtype, int flags, const GemmParams& p, int S, float* part,
+                              hipStream_t s);
 void gemm_set_variant(int v);
 // Bytes of the stream-K scratch of one GEMM stream (flags block first, zero it once after
 // allocating: the kernel leaves every flag at 0); gemm_sk_bind splits it into the two arrays.

@@ -399,6 +399,13 @@ __device__ __forceinline__ void epi_rows(const GemmParams& p, EVT_LDS char* stg,
 template <typename T, int FL>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+  if (gridDim.y > 1) {  // split-K (gemm_splitk_launch): this block's K range and partial C
+    const int z = blockIdx.y;
+    p.A = (const T*)p.A + (int64_t)z * p.ks_chunk;
+    p.W = (const T*)p.W + (int64_t)z * p.ks_chunk;
+    p.K = p.ks_chunk;
+    p.C = (float*)p.C + (int64_t)z * p.ks_stride;
+  }
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably uniform -> SGPR math
@@ -1699,6 +1706,58 @@ hipError_t dispatch(int flags, const GemmParams& p, hipStream_t s) {
   }
 }
 
+// out[m][n] = epilogue(sum_z part[z][m][n] + bias[n]), z in order (4 columns per thread)
+template <typename T, bool GELU>
+__global__ void splitk_reduce_kernel(const float* __restrict__ part, int S, int64_t stride,
+                                     int ldp, const float* __restrict__ bias, T* __restrict__ out,
+                                     int64_t ldo, int M, int N) {
+  const int n4 = (N + 3) >> 2;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)M * n4) return;
+  const int m = (int)(i / n4), n = (int)(i - (int64_t)m * n4) * 4;
+  f32x4 v = *(const f32x4*)(part + (int64_t)m * ldp + n);
+  for (int z = 1; z < S; ++z) v += *(const f32x4*)(part + z * stride + (int64_t)m * ldp + n);
+  if (bias) v += *(const f32x4*)(bias + n);  // bias: >= ntiles*128 floats (zero padded)
+  if (GELU) v = gelu4(v, 0);
+  for (int j = 0; j < 4; ++j)
+    if (n + j < N) out[(int64_t)m * ldo + n + j] = (T)v[j];
+}
+
+template <typename T>
+hipError_t splitk_t(int flags, const GemmParams& p, int S, float* part, hipStream_t s) {
+  GemmParams q = p;
+  const int ldp = p.ntiles * GEMM_BN;
+  q.ks_chunk = p.K / S;
+  q.ks_stride = (int64_t)p.M * ldp;
+  q.C = part;
+  q.ldc = ldp;
+  q.N = ldp;
+  q.vec_ok = 2;
+  q.bias = nullptr;
+  const int mtiles = (p.M + GEMM_BM - 1) / GEMM_BM;
+  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_OUT_F32>), dim3(mtiles * p.ntiles, S), dim3(256), 0, s, q);
+  const int64_t n = (int64_t)p.M * ((p.N + 3) / 4);
+  const dim3 grid((unsigned)((n + 255) / 256));
+  const bool gelu = (flags & EPI_GELU) != 0;
+  if (flags & EPI_OUT_F32) {
+    if (gelu)
+      hipLaunchKernelGGL((splitk_reduce_kernel<float, true>), grid, dim3(256), 0, s, part, S,
+                         q.ks_stride, ldp, p.bias, (float*)p.C, p.ldc, p.M, p.N);
+    else
+      hipLaunchKernelGGL((splitk_reduce_kernel<float, false>), grid, dim3(256), 0, s, part, S,
+                         q.ks_stride, ldp, p.bias, (float*)p.C, p.ldc, p.M, p.N);
+  } else {
+    if (gelu)
+      hipLaunchKernelGGL((splitk_reduce_kernel<T, true>), grid, dim3(256), 0, s, part, S,
+                         q.ks_stride, ldp, p.bias, (T*)p.C, p.ldc, p.M, p.N);
+    else
+      hipLaunchKernelGGL((splitk_reduce_kernel<T, false>), grid, dim3(256), 0, s, part, S,
+                         q.ks_stride, ldp, p.bias, (T*)p.C, p.ldc, p.M, p.N);
+  }
+  return hipGetLastError();
+}
+
+
 // Wp[n][k] = W[k][n] * (scale ? scale[k] : 1) (fp32 [K][N] in) converted to T, zero outside
 // [N) x [K). `scale` folds a LayerNorm gamma into the weight rows.
 template <typename T>
@@ -1759,6 +1818,14 @@ hipError_t gemm_launch(int dtype, int flags, const GemmParams& p, hipStream_t s)
   if (p.K % PAD_K != 0 || p.K <= 0) return hipErrorInvalidValue;
   if (p.ntiles * GEMM_BN < p.N) return hipErrorInvalidValue;
   return dtype == DT_BF16 ? dispatch<bf16>(flags, p, s) : dispatch<float>(flags, p, s);
+}
+
+hipError_t gemm_splitk_launch(int dtype, int flags, const GemmParams& p, int S, float* part,
+                              hipStream_t s) {
+  if (p.M <= 0 || p.N <= 0) return hipSuccess;
+  if (S < 1 || p.K % (S * PAD_K) || (flags & ~(EPI_BIAS | EPI_GELU | EPI_OUT_F32)) || !part)
+    return hipErrorInvalidValue;
+  return dtype == DT_BF16 ? splitk_t<bf16>(flags, p, S, part, s) : splitk_t<float>(flags, p, S, part, s);
 }
 
 hipError_t pack_weight(int dtype, const float* W, const float* row_scale, int K, int N, void* Wp,
