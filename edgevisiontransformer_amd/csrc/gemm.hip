@@ -601,10 +601,13 @@ __device__ __forceinline__ void big8_prologue(const GemmParams& p, char* smem, i
 // One K-tile. MODE 0 steady (all DMAs, waits 8), 1 second-to-last tile, 2 last tile. X is
 // added to every wait of the tile: the number of VMEM instructions each wave is known to have
 // issued after the prologue DMAs (gemm_pers_kernel's epilogue stores; first K-tile only).
+// cont (persistent kernel, even nk): the last 1.5 K-tiles' DMA slots, idle otherwise, carry the
+// NEXT tile's prologue (its K-tiles 0 and 1 are this tile's K-tiles nk and nk + 1 of one continuous
+// stream: same buffers, same WAR distances, the steady-state waits), at (nm0, nn0).
 template <int MODE, int X>
 __device__ __forceinline__ void big8_ktile(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
                                            int wave, int lane, int wm, int wn, int m0, int n0,
-                                           int t) {
+                                           int t, bool cont = false, int nm0 = 0, int nn0 = 0) {
   const int frow = lane & 15, fsw = lane & 7, fg = lane >> 4;
   const EVT_LDS char* As = (const EVT_LDS char*)smem + (t & 1) * BIG_STAGE;
   const EVT_LDS char* Ws = As + BIG_TILE;
@@ -638,11 +641,16 @@ __device__ __forceinline__ void big8_ktile(const GemmParams& p, char* smem, f32x
     if (MODE == 0 || (MODE == 1 && ph < 2)) {
       if (ph < 2) big8_stage(p, smem, wave, lane, m0, n0, t + 1, ph + 2);
       else big8_stage(p, smem, wave, lane, m0, n0, t + 2, ph - 2);
+    } else if (cont) {  // MODE 1 phases 2, 3 and MODE 2: the next tile's regions, in order
+      const int s6 = (MODE == 1 ? ph - 2 : ph + 2);  // 0..5: (K-tile 0, regions 0-3), (1, 0-1)
+      big8_stage(p, smem, wave, lane, nm0, nn0, s6 >> 2, s6 & 3);
     }
     // retire what the next phase reads (phases 4, 1, 2 precede reading phases)
     if (ph != 2) {
       if (MODE == 0) wait_vm<8 + X>();
-      else if (MODE == 1) {
+      else if (cont) {  // the steady-state DMA pattern continues: steady-state waits
+        wait_vm<8 + X>();
+      } else if (MODE == 1) {
         if (ph == 3) wait_vm<4 + X>();
         else wait_vm<8 + X>();
       } else if (ph == 0) {
@@ -673,7 +681,7 @@ __device__ __forceinline__ void big8_ktile(const GemmParams& p, char* smem, f32x
 template <int X>
 __device__ __forceinline__ void big8_loop(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
                                           int wave, int lane, int wm, int wn, int m0, int n0,
-                                          int nk) {
+                                          int nk, bool cont = false, int nm0 = 0, int nn0 = 0) {
   if (nk >= 2) wait_vm<8 + X>();
   else wait_vm<4 + X>();
   big8_bar();
@@ -682,11 +690,11 @@ __device__ __forceinline__ void big8_loop(const GemmParams& p, char* smem, f32x4
     big8_ktile<0, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0);
     int t = 1;
     for (; t + 2 < nk; ++t) big8_ktile<0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t);
-    big8_ktile<1, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t);
-    big8_ktile<2, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1);
+    big8_ktile<1, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, cont, nm0, nn0);
+    big8_ktile<2, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1, cont, nm0, nn0);
   } else if (nk == 2) {
-    big8_ktile<1, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0);
-    big8_ktile<2, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, 1);
+    big8_ktile<1, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, cont, nm0, nn0);
+    big8_ktile<2, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, 1, cont, nm0, nn0);
   } else {
     big8_ktile<2, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0);
   }
@@ -1386,19 +1394,23 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
       for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     int ln = lane;
     asm volatile("" : "+v"(ln));  // per-tile lane addresses: not hoisted out of the tile loop
-    big8_loop<PERS_X>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk);
-    stamp(1);
-    pers_coef<FL>(p, smem, tid);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    big8_bar();
     const int next = tile + G;
     const bool has_next = next < total;
     int ntm = 0, ntn = 0;
     if (has_next) {
       ntm = next / p.ntiles;
       ntn = next - ntm * p.ntiles;
+    }
+    // even nk: the next tile's prologue rides in the last K-tiles' idle DMA slots (big8_ktile)
+    const bool cont = has_next && !(nk & 1) && DBG != 16;
+    big8_loop<PERS_X>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM, ntn * BIG_BN);
+    stamp(1);
+    pers_coef<FL>(p, smem, tid);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    big8_bar();
+    if (has_next) {
       pers_coop_dma<FL>(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN);
-      big8_prologue(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nk);
+      if (!cont) big8_prologue(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nk);
     }
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -1606,7 +1618,7 @@ constexpr bool pers_fl(int fl) {
 
 // persistent kernel: supported epilogue, 8-column output groups, LN rows of <= 8 slots
 bool use_pers(const GemmParams& p, int flags) {
-  if (g_gemm_variant != 0 && (g_gemm_variant < 9 || g_gemm_variant > 20 || g_gemm_variant == 12 ||
+  if (g_gemm_variant != 0 && (g_gemm_variant < 9 || g_gemm_variant > 21 || g_gemm_variant == 12 ||
                               g_gemm_variant == 14))
     return false;
   if (p.N % 8 || p.vec_ok < 2) return false;
@@ -1633,6 +1645,8 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 6, false>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 17)  // ablation: main loop + tile loop only (no epilogue)
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 2, false>), dim3(G), dim3(512), 0, s, q, total);
+  else if (g_gemm_variant == 21)  // A/B: next-tile prologue issued after the main loop
+    hipLaunchKernelGGL((gemm_pers_kernel<FL, 16, false>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 20)  // ablation: no residual loads (out-proj 153 -> 115 us)
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 7, false>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 18)  // ablation: epilogue without the GELU
