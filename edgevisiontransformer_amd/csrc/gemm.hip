@@ -678,16 +678,27 @@ __device__ __forceinline__ void big8_ktile(const GemmParams& p, char* smem, f32x
 
 // Main loop over the nk K-tiles after big8_prologue (whose DMAs may be followed by X further
 // VMEM instructions per wave, or by a vmcnt(0)). Ends with every wave past a common barrier.
-template <int X>
+struct NoOp {
+  __device__ void operator()() const {}
+};
+
+// pre1: run by wave group 1 in the slot where it waits one barrier for group 0 (per-tile LDS
+// setup work that is then off the critical path); mid: after K-tile 0 (nk >= 3 only).
+template <int X, typename Pre1 = NoOp, typename Mid = NoOp>
 __device__ __forceinline__ void big8_loop(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
                                           int wave, int lane, int wm, int wn, int m0, int n0,
-                                          int nk, bool cont = false, int nm0 = 0, int nn0 = 0) {
+                                          int nk, bool cont = false, int nm0 = 0, int nn0 = 0,
+                                          Pre1 pre1 = {}, Mid mid = {}) {
   if (nk >= 2) wait_vm<8 + X>();
   else wait_vm<4 + X>();
   big8_bar();
-  if (wm == 1) big8_bar();
+  if (wm == 1) {
+    pre1();
+    big8_bar();
+  }
   if (nk >= 3) {
     big8_ktile<0, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0);
+    mid();
     int t = 1;
     for (; t + 2 < nk; ++t) big8_ktile<0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t);
     big8_ktile<1, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, cont, nm0, nn0);
@@ -1379,6 +1390,8 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
   pers_coop_dma<FL>(p, smem, wave, lane, tm * BIG_BM, tn * BIG_BN);
   big8_prologue(p, smem, wave, lane, tm * BIG_BM, tn * BIG_BN, nk);
   wait_vmcnt0();  // the first K-tile's waits assume PERS_X younger VMEM ops or a drain
+  // nk >= 3: per-tile LayerNorm coefficients / next statistics DMA inside the main loop
+  const bool early = nk >= 3 && DBG != 16 && DBG != 17;
   int iter = 0;
   auto stamp = [&](int k) {  // DBG 3: timeline of block's tiles (s_memtime, wave 0)
     if ((DBG == 3 || DBG == 5) && tid == 0 && iter < 16)
@@ -1403,14 +1416,28 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
     }
     // even nk: the next tile's prologue rides in the last K-tiles' idle DMA slots (big8_ktile)
     const bool cont = has_next && !(nk & 1) && DBG != 16;
-    big8_loop<PERS_X>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM, ntn * BIG_BN);
-    stamp(1);
-    pers_coef<FL>(p, smem, tid);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    big8_bar();
-    if (has_next) {
-      pers_coop_dma<FL>(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN);
-      if (!cont) big8_prologue(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nk);
+    if (early) {
+      // this tile's LayerNorm coefficients by wave group 1 while it waits for group 0's first
+      // phase; the next tile's statistics rows / column vectors DMA'd after K-tile 0 (PERS_RAW is
+      // free once those coefficients are read: every later phase retires group 1's LDS ops)
+      auto pre1 = [&]() { pers_coef<FL>(p, smem, tid - 256); };
+      auto mid = [&]() {
+        if (has_next) pers_coop_dma<FL>(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN);
+      };
+      big8_loop<PERS_X>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
+                        ntn * BIG_BN, pre1, mid);
+      stamp(1);
+      if (has_next && !cont) big8_prologue(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nk);
+    } else {
+      big8_loop<PERS_X>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM, ntn * BIG_BN);
+      stamp(1);
+      pers_coef<FL>(p, smem, tid);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      big8_bar();
+      if (has_next) {
+        pers_coop_dma<FL>(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN);
+        if (!cont) big8_prologue(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nk);
+      }
     }
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -1618,7 +1645,7 @@ constexpr bool pers_fl(int fl) {
 
 // persistent kernel: supported epilogue, 8-column output groups, LN rows of <= 8 slots
 bool use_pers(const GemmParams& p, int flags) {
-  if (g_gemm_variant != 0 && (g_gemm_variant < 9 || g_gemm_variant > 21 || g_gemm_variant == 12 ||
+  if (g_gemm_variant != 0 && (g_gemm_variant < 9 || g_gemm_variant > 22 || g_gemm_variant == 12 ||
                               g_gemm_variant == 14))
     return false;
   if (p.N % 8 || p.vec_ok < 2) return false;
@@ -1645,6 +1672,8 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 6, false>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 17)  // ablation: main loop + tile loop only (no epilogue)
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 2, false>), dim3(G), dim3(512), 0, s, q, total);
+  else if (g_gemm_variant == 22)  // A/B: LN coefficients / statistics DMA after the main loop
+    hipLaunchKernelGGL((gemm_pers_kernel<FL, 17, false>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 21)  // A/B: next-tile prologue issued after the main loop
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 16, false>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 20)  // ablation: no residual loads (out-proj 153 -> 115 us)
