@@ -604,7 +604,10 @@ __device__ __forceinline__ void big8_prologue(const GemmParams& p, char* smem, i
 // cont (persistent kernel, even nk): the last 1.5 K-tiles' DMA slots, idle otherwise, carry the
 // NEXT tile's prologue (its K-tiles 0 and 1 are this tile's K-tiles nk and nk + 1 of one continuous
 // stream: same buffers, same WAR distances, the steady-state waits), at (nm0, nn0).
-template <int MODE, int X>
+// OPEN (last K-tile of a persistent-kernel tile): wave group 1 skips the barrier that closes its
+// final MFMA phase and group 0 the resync barrier after the loop, so group 0 starts its epilogue
+// while group 1 still issues its last 16 MFMAs (the two barriers cancel in every wave's count).
+template <int MODE, int X, bool OPEN = false>
 __device__ __forceinline__ void big8_ktile(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
                                            int wave, int lane, int wm, int wn, int m0, int n0,
                                            int t, bool cont = false, int nm0 = 0, int nn0 = 0) {
@@ -672,7 +675,7 @@ __device__ __forceinline__ void big8_ktile(const GemmParams& p, char* smem, f32x
         for (int mt = 0; mt < 4; ++mt)
           Mma<bf16>::run(nb ? bf1[nt][ks] : bf0[nt][ks], af[mt][ks], acc[nb + nt][mb + mt]);
     __builtin_amdgcn_s_setprio(0);
-    big8_bar();
+    if (!(OPEN && MODE == 2 && ph == 3 && wm == 1)) big8_bar();
   }
 }
 
@@ -684,7 +687,7 @@ struct NoOp {
 
 // pre1: run by wave group 1 in the slot where it waits one barrier for group 0 (per-tile LDS
 // setup work that is then off the critical path); mid: after K-tile 0 (nk >= 3 only).
-template <int X, typename Pre1 = NoOp, typename Mid = NoOp>
+template <int X, bool OPEN = false, typename Pre1 = NoOp, typename Mid = NoOp>
 __device__ __forceinline__ void big8_loop(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
                                           int wave, int lane, int wm, int wn, int m0, int n0,
                                           int nk, bool cont = false, int nm0 = 0, int nn0 = 0,
@@ -702,14 +705,14 @@ __device__ __forceinline__ void big8_loop(const GemmParams& p, char* smem, f32x4
     int t = 1;
     for (; t + 2 < nk; ++t) big8_ktile<0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t);
     big8_ktile<1, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, cont, nm0, nn0);
-    big8_ktile<2, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1, cont, nm0, nn0);
+    big8_ktile<2, 0, OPEN>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1, cont, nm0, nn0);
   } else if (nk == 2) {
     big8_ktile<1, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, cont, nm0, nn0);
-    big8_ktile<2, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, 1, cont, nm0, nn0);
+    big8_ktile<2, 0, OPEN>(p, smem, acc, wave, lane, wm, wn, m0, n0, 1, cont, nm0, nn0);
   } else {
-    big8_ktile<2, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0);
+    big8_ktile<2, X, OPEN>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0);
   }
-  if (wm == 0) big8_bar();
+  if (!OPEN && wm == 0) big8_bar();
 }
 
 template <int FL, int VAR_, bool NOEPI = false>
@@ -1424,8 +1427,12 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
       auto mid = [&]() {
         if (has_next) pers_coop_dma<FL>(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN);
       };
-      big8_loop<PERS_X>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
-                        ntn * BIG_BN, pre1, mid);
+      if constexpr (DBG == 18)  // A/B: groups re-synchronised before the epilogue
+        big8_loop<PERS_X>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
+                          ntn * BIG_BN, pre1, mid);
+      else
+        big8_loop<PERS_X, true>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
+                                ntn * BIG_BN, pre1, mid);
       stamp(1);
       if (has_next && !cont) big8_prologue(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nk);
     } else {
@@ -1645,7 +1652,7 @@ constexpr bool pers_fl(int fl) {
 
 // persistent kernel: supported epilogue, 8-column output groups, LN rows of <= 8 slots
 bool use_pers(const GemmParams& p, int flags) {
-  if (g_gemm_variant != 0 && (g_gemm_variant < 9 || g_gemm_variant > 22 || g_gemm_variant == 12 ||
+  if (g_gemm_variant != 0 && (g_gemm_variant < 9 || g_gemm_variant > 23 || g_gemm_variant == 12 ||
                               g_gemm_variant == 14))
     return false;
   if (p.N % 8 || p.vec_ok < 2) return false;
@@ -1672,6 +1679,8 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 6, false>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 17)  // ablation: main loop + tile loop only (no epilogue)
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 2, false>), dim3(G), dim3(512), 0, s, q, total);
+  else if (g_gemm_variant == 23)  // A/B: wave groups re-synchronised before the epilogue
+    hipLaunchKernelGGL((gemm_pers_kernel<FL, 18, false>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 22)  // A/B: LN coefficients / statistics DMA after the main loop
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 17, false>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 21)  // A/B: next-tile prologue issued after the main loop
