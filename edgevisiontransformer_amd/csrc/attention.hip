@@ -215,7 +215,7 @@ __device__ __forceinline__ void attn_tile_bf16(const AttnParams& p, const EVT_LD
 
 // Stage one (image, head)'s K and V rows (NP rows, clamped past N) into LDS with glds, WAVES
 // waves sharing the rows, and load the Q fragments of query tiles wave, wave + WAVES, ...
-template <int NKT, int WAVES, int NQW>
+template <int NKT, int WAVES, int NQW, bool NT = false, bool NTQ = NT>
 __device__ __forceinline__ void attn_stage_bf16(const AttnParams& p, EVT_LDS char* Ks,
                                                 EVT_LDS char* Vs, u32x4 (&qf)[NQW][2], int b,
                                                 int h, int wave, int lane) {
@@ -226,21 +226,31 @@ __device__ __forceinline__ void attn_stage_bf16(const AttnParams& p, EVT_LDS cha
   for (int i = 0; i < NQW; ++i) {
     const int qi = min((wave + WAVES * i) * 16 + c16, p.N - 1);
     const bf16* qrow = qkv + (int64_t)qi * p.ldq + h * 64;
-    qf[i][0] = *(const u32x4*)(qrow + 8 * g);
-    qf[i][1] = *(const u32x4*)(qrow + 8 * (g + 4));
+    if (NTQ) {
+      qf[i][0] = __builtin_nontemporal_load((const u32x4*)(qrow + 8 * g));
+      qf[i][1] = __builtin_nontemporal_load((const u32x4*)(qrow + 8 * (g + 4)));
+    } else {
+      qf[i][0] = *(const u32x4*)(qrow + 8 * g);
+      qf[i][1] = *(const u32x4*)(qrow + 8 * (g + 4));
+    }
   }
   const int srow = lane >> 3, sslot = lane & 7;  // 8 rows of 128 B per wave-instruction
   for (int i = wave; i < NP / 8; i += WAVES) {
     const int row = i * 8 + srow;
     const int gr = min(row, p.N - 1);
     const bf16* rp = qkv + (int64_t)gr * p.ldq + ((sslot ^ srow) * 8);
-    glds16(rp + (p.H + h) * 64, Ks + i * 8 * ROWB);
-    glds16(rp + (2 * p.H + h) * 64, Vs + i * 8 * ROWB);
+    if (NT) {
+      __builtin_amdgcn_global_load_lds(rp + (p.H + h) * 64, Ks + i * 8 * ROWB, 16, 0, 2);
+      __builtin_amdgcn_global_load_lds(rp + (2 * p.H + h) * 64, Vs + i * 8 * ROWB, 16, 0, 2);
+    } else {
+      glds16(rp + (p.H + h) * 64, Ks + i * 8 * ROWB);
+      glds16(rp + (2 * p.H + h) * 64, Vs + i * 8 * ROWB);
+    }
   }
 }
 
 // One workgroup (4 waves) per (image, head); 3 per CU (53 KiB of LDS each).
-template <int NKT>  // 16-key tiles (keys padded to NKT*16; odd NKT: a half last PV step)
+template <int NKT, int NTM = 0>  // 16-key tiles (keys padded to NKT*16; odd NKT: a half last PV step)
 __global__ __launch_bounds__(256, (NKT == 13 || NKT == 12) ? 3 : 1) void attn_bf16_kernel(AttnParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NP = NKT * 16, ROWB = 128;
@@ -251,14 +261,17 @@ __global__ __launch_bounds__(256, (NKT == 13 || NKT == 12) ? 3 : 1) void attn_bf
   const int b = blockIdx.x / p.H, h = blockIdx.x - b * p.H;
   const int nqt = (p.N + 15) >> 4;
   u32x4 qf[NQW][2];
-  attn_stage_bf16<NKT, 4, NQW>(p, Ks, Vs, qf, b, h, wave, lane);
+  // NTM: cache policy of the qkv loads / O stores, non-temporal for 1 all, 2 K/V loads only, 3 O
+  // stores only, 4 K/V + Q loads only, 5 K/V loads + O stores (the launched form)
+  attn_stage_bf16<NKT, 4, NQW, (NTM == 1 || NTM == 2 || NTM == 4 || NTM == 5), (NTM == 1 || NTM == 4)>(
+      p, Ks, Vs, qf, b, h, wave, lane);
   wait_vmcnt0();
   __syncthreads();
 #pragma unroll
   for (int it = 0; it < NQW; ++it) {
     const int qt = wave + 4 * it;
     if (qt >= nqt) break;
-    attn_tile_bf16<NKT, true>(p, Ks, Vs, qf[it][0], qf[it][1], qt, b, h, lane);
+    attn_tile_bf16<NKT, !(NTM == 1 || NTM == 3 || NTM == 5)>(p, Ks, Vs, qf[it][0], qf[it][1], qt, b, h, lane);
   }
 }
 
@@ -366,8 +379,11 @@ template <int NKT>
 hipError_t launch_nkt(int dtype, const AttnParams& p, hipStream_t s) {
   const int rowb = dtype == DT_BF16 ? 128 : 256;
   const size_t lds = 2 * (size_t)NKT * 16 * rowb;
+  // K / V loads and O stores non-temporal (NTM 5): measured in the model, out-proj (whose A is O
+  // and whose residual x was read by the QKV GEMM just before) 161 -> 157 us and attention equal
+  // or 2 us faster; all-NT (Q too) made attention 4 us slower (scripts/gpu_attnnt.sh)
   if (dtype == DT_BF16)
-    hipLaunchKernelGGL(attn_bf16_kernel<NKT>, dim3(p.B * p.H), dim3(256), lds, s, p);
+    hipLaunchKernelGGL((attn_bf16_kernel<NKT, 5>), dim3(p.B * p.H), dim3(256), lds, s, p);
   else if constexpr (NKT % 2 == 0)
     hipLaunchKernelGGL(attn_f32_kernel<NKT>, dim3(p.B * p.H), dim3(256), lds, s, p);
   else
