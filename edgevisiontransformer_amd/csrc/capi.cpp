@@ -120,6 +120,7 @@ struct evt_model {
   Shape sh;
   DenseW patch, head1, head2;
   float *cls = nullptr, *pos = nullptr;
+  void* pos_h = nullptr;     // bf16 copy of pos (the persistent patch-embedding GEMM's EPI_POS)
   std::vector<Layer> layers;
   std::vector<void*> allocs;
   // T2T stage
@@ -792,6 +793,10 @@ int evt_vit_create(const evt_vit_desc* desc, const float* const* w, int n_weight
     }
     EVT_RC(copy_vec(m, &m->cls, w[2], D, s));
     EVT_RC(copy_vec(m, &m->pos, w[3], (size_t)sh.T * D, s));
+    if (m->dtype == DT_BF16) {
+      EVT_RC(dev_alloc(m, &m->pos_h, (size_t)sh.T * D * 2));
+      EVT_HIP(to_bf16_launch(m->pos, m->pos_h, (int64_t)sh.T * D, s), "pos -> bf16");
+    }
     EVT_RC(build_encoder(m, w + 4, s));
     const int k = 4 + (m->standard ? 12 : 11) * desc->depth;
     if (m->standard) {  // final LayerNorm folded into the classifier (CLS rows)
@@ -855,6 +860,7 @@ int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* 
     c.flags = EPI_BIAS | EPI_POS | EPI_STATS;
     c.A = m->apatch; c.lda = sh.pd; c.C = m->x; c.ldc = D; c.M = B * sh.P; c.N = D;
     c.pos = m->pos; c.ldp = D; c.P = sh.P; c.stats_out = m->sx;
+    c.resid = m->pos_h; c.ldr = m->pos_h ? D : 0;  // bf16 table for the persistent kernel
     EVT_RC(dense(m, m->patch, c, s));
   }
   EVT_RC(m->mx8 ? run_encoder_mx8(m, B, s) : run_encoder(m, B, s));
@@ -1439,7 +1445,7 @@ int evt_dense(int dtype, const evt_dense_args* a, void* stream) {
   const int f = a->flags;
   if ((f & EPI_BIAS) && !a->bias) return fail(EVT_EINVAL, "dense: bias flag without bias");
   if ((f & EPI_RESID) && (!a->resid || a->ldr < a->N)) return fail(EVT_EINVAL, "dense: bad resid");
-  if ((f & EPI_POS) && (!a->pos || a->P <= 0 || a->ldp < a->N))
+  if ((f & EPI_POS) && (!a->pos || a->P <= 0 || a->ldp < a->N || (a->resid && a->ldr < a->N)))
     return fail(EVT_EINVAL, "dense: bad pos");
   if ((f & EPI_LNIN) && (!a->colsum || !a->stats_in || a->ln_width <= 0))
     return fail(EVT_EINVAL, "dense: LN-in needs colsum, stats_in, ln_width");

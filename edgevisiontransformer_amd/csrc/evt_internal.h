@@ -70,6 +70,7 @@ size_t gemm_sk_bytes();
 void gemm_sk_bind(void* ws, GemmParams& p);  // 0 auto, 1 force 128x128 tiles, 2 force 256x256 (bf16)
 hipError_t pack_weight(int dtype, const float* W, const float* row_scale, int K, int N, void* Wp,
                        int Kpad, int Npad, hipStream_t s);
+hipError_t to_bf16_launch(const float* x, void* y, int64_t n, hipStream_t s);  // y[i] = bf16(x[i])
 // colsum[n] = sum_k Wp[n][k]; cvec[n] = sum_k beta[k] W[k][n] + bias[n] (bias may be null).
 hipError_t ln_fold(int dtype, const void* Wp, int Kpad, const float* W, const float* beta,
                    const float* bias, int K, int N, float* colsum, float* cvec, int Npad,

@@ -868,7 +868,10 @@ struct PersFlags {
   static_assert(!((FL & EPI_LNIN) && (FL & EPI_RESLN)), "one LayerNorm source per GEMM");
   static_assert(!(FL & EPI_RESLN) || ((FL & EPI_BIAS) && (FL & EPI_RESID)),
                 "RESLN: the residual LayerNorm's beta is folded into the bias add");
-  static_assert(!(FL & (EPI_POS | EPI_OUT_F32)), "persistent kernel: bf16 outputs, no EPI_POS");
+  static_assert(!(FL & EPI_OUT_F32), "persistent kernel: bf16 outputs");
+  // EPI_POS (patch embedding): + pos[t + 1][n] from a bf16 copy of the table in p.resid (pitch
+  // p.ldr), row remap b*P + t -> b*(P+1) + 1 + t of the outputs and their statistics
+  static_assert(!(FL & EPI_POS) || !(FL & (EPI_RESID | EPI_LNIN)), "POS: its own residual form");
 };
 
 // DMA the tile's LN statistics rows and column vectors into LDS (before its prologue DMAs).
@@ -1142,6 +1145,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* mat, int
                                            0, nr, 0x00020000);
 }
 
+// EPI_POS row arithmetic: image of patch row m (m / P, exact in fp32 for m < 2^22 with the
+// half-row offset) and its token row in the stream, b*(P+1) + 1 + t = m + m/P + 1.
+__device__ __forceinline__ int pos_img(int m, int P) {
+  return (int)(((float)m + 0.5f) * (1.0f / (float)P));
+}
+__device__ __forceinline__ int pos_orow(int m, int P) { return m + pos_img(m, P) + 1; }
+
 // Epilogue of one 256 x 256 tile straight from the accumulators (VALU-bound: every instruction
 // here is paid with the MFMA pipe idle, so the arithmetic is in packed form throughout):
 //   LNIN   r (acc - mu colsum) + c      2 v_pk_fma per column pair
@@ -1256,6 +1266,18 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
       for (int nt = 0; nt < 4; ++nt)
         rr[k][nt] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 32 * nt, so, 0));
     }
+  } else if constexpr ((FL & EPI_POS) != 0) {  // pos[t + 1][n0 + cl + 16 nt ..] (bf16 table)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(p.resid), 0, (p.P + 1) * (int)p.ldr * 2, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int m = min(m0 + rl + 32 * k, p.M - 1);
+      const int t = m - pos_img(m, p.P) * p.P;
+      const int vo = ((t + 1) * (int)p.ldr + n0 + cl) * 2;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        rr[k][nt] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 32 * nt, 0, 0));
+    }
   }
   f32x2 rc[4], st[4];
   u32x4 ov[4][4];
@@ -1276,7 +1298,7 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       f32x4 v[2] = {acc[nt][2 * k], acc[nt][2 * k + 1]};
-      if constexpr ((FL & EPI_RESID) != 0) {
+      if constexpr ((FL & (EPI_RESID | EPI_POS)) != 0) {
         const bf16x8 r8 = __builtin_bit_cast(bf16x8, rr[k][nt]);
         const f32x2 rrow = {rc[k][1], rc[k][1]}, nrm = {-rc[k][1] * rc[k][0], -rc[k][1] * rc[k][0]};
 #pragma unroll
@@ -1323,8 +1345,17 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
     const int wrow = (fg & 1) * 16 + frow;               // store-layout row within the pair
     const int rrow = lane >> 3, rch = lane & 7;          // row-layout lane: row i*8 + rrow, chunk
     const bool rcol_ok = !PADN || interior || n0 + wn * 64 + rch * 8 < p.N;
-    const __amdgpu_buffer_rsrc_t cs = tile_rsrc(p.C, p.ldc, p.M, m0, n0);
-    const int vo = ((wm * 128 + rrow) * (int)p.ldc + wn * 64 + rch * 8) * 2;
+    __amdgpu_buffer_rsrc_t cs;
+    int vo = ((wm * 128 + rrow) * (int)p.ldc + wn * 64 + rch * 8) * 2, orow0 = 0;
+    if constexpr ((FL & EPI_POS) != 0) {  // output rows b*(P+1) + 1 + t, base at tile row 0
+      orow0 = __builtin_amdgcn_readfirstlane(pos_orow(m0, p.P));
+      const int olast = pos_orow(min(m0 + BIG_BM, p.M) - 1, p.P);
+      const int nr = ((olast + 1 - orow0) * (int)p.ldc - n0) * 2;
+      cs = __builtin_amdgcn_make_buffer_rsrc((char*)p.C + ((int64_t)orow0 * p.ldc + n0) * 2, 0,
+                                             nr, 0x00020000);
+    } else {
+      cs = tile_rsrc(p.C, p.ldc, p.M, m0, n0);
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
 #pragma unroll
@@ -1341,9 +1372,14 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
         if (DBG == 1) {  // ablation: no stores, every value stays live
           keep = (v[0] ^ v[1] ^ v[2] ^ v[3]) == 0x12345u;
         }
-        const int so = __builtin_amdgcn_readfirstlane((32 * k + 8 * i) * (int)p.ldc * 2);
+        int so = __builtin_amdgcn_readfirstlane((32 * k + 8 * i) * (int)p.ldc * 2), svo = vo;
+        if constexpr ((FL & EPI_POS) != 0) {  // per-lane remapped row (rows past M: beyond nr)
+          so = 0;
+          svo = ((pos_orow(m0 + wm * 128 + 32 * k + 8 * i + rrow, p.P) - orow0) * (int)p.ldc +
+                 wn * 64 + rch * 8) * 2;
+        }
         if (keep)  // nontemporal (aux nt): whole lines streamed past L2
-          __builtin_amdgcn_raw_buffer_store_b128(v, cs, vo, so, 2);
+          __builtin_amdgcn_raw_buffer_store_b128(v, cs, svo, so, 2);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
@@ -1368,8 +1404,9 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
       for (int k = 0; k < 4; ++k) {
         const int m = m0 + rl + 32 * k;
         const f32x2 o = part[rl + 32 * k];
+        const int sm = (FL & EPI_POS) ? pos_orow(m, p.P) : m;
         if (interior || m < p.M)
-          *(f32x2*)(p.stats_out + 2 * ((int64_t)p.nslots * m + 2 * tn + (wn >> 1))) = st[k] + o;
+          *(f32x2*)(p.stats_out + 2 * ((int64_t)p.nslots * sm + 2 * tn + (wn >> 1))) = st[k] + o;
       }
     }
   }
@@ -1644,6 +1681,7 @@ int num_cus() {
 
 constexpr bool pers_fl(int fl) {
   return fl == 0 || fl == EPI_BIAS || fl == (EPI_BIAS | EPI_GELU) || fl == (EPI_LNIN | EPI_BIAS) ||
+         fl == (EPI_BIAS | EPI_POS | EPI_STATS) ||
          fl == (EPI_LNIN | EPI_BIAS | EPI_GELU) ||
          fl == (EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS) ||
          fl == (EPI_LNIN | EPI_BIAS | EPI_GELU_ERF) || fl == (EPI_BIAS | EPI_RESID | EPI_STATS) ||
@@ -1658,6 +1696,8 @@ bool use_pers(const GemmParams& p, int flags) {
   if (p.N % 8 || p.vec_ok < 2) return false;
   if ((flags & (EPI_LNIN | EPI_RESLN)) && (p.nslots > 8 || p.nslots % 2 || p.stats_step > 1))
     return false;
+  // POS: the bf16 copy of the position table rides in resid / ldr (else the staged-epilogue kernel)
+  if ((flags & EPI_POS) && (!p.resid || p.ldr % 8 || p.P <= 0 || p.M >= (1 << 22))) return false;
   return true;
 }
 
@@ -1878,6 +1918,19 @@ hipError_t gemm_splitk_launch(int dtype, int flags, const GemmParams& p, int S, 
   if (S < 1 || p.K % (S * PAD_K) || (flags & ~(EPI_BIAS | EPI_GELU | EPI_OUT_F32)) || !part)
     return hipErrorInvalidValue;
   return dtype == DT_BF16 ? splitk_t<bf16>(flags, p, S, part, s) : splitk_t<float>(flags, p, S, part, s);
+}
+
+namespace {
+__global__ void to_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = (bf16)x[i];
+}
+}  // namespace
+
+hipError_t to_bf16_launch(const float* x, void* y, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(to_bf16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, (bf16*)y, n);
+  return hipGetLastError();
 }
 
 hipError_t pack_weight(int dtype, const float* W, const float* row_scale, int K, int N, void* Wp,

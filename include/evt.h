@@ -186,7 +186,8 @@ typedef struct evt_dense_args {
   void* C;         int64_t ldc;     /* [M, N] (fp32 with EVT_EPI_OUT_F32) */
   int32_t M, N;
   const float* bias;                /* >= N floats */
-  const void* resid; int64_t ldr;   /* activation dtype */
+  const void* resid; int64_t ldr;   /* activation dtype; with EVT_EPI_POS (bf16): optional bf16
+                                       copy of pos [P+1][ldr] (the persistent-kernel path) */
   const float* pos;  int64_t ldp;  int32_t P;
   const float* colsum;              /* EVT_EPI_LNIN */
   const float* stats_in;            /* EVT_EPI_LNIN: [M][S][2] slot statistics of the A rows */

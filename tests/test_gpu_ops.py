@@ -100,6 +100,37 @@ def test_dense_patch_embed_remap(gpu, dtype):
     torch.testing.assert_close(got[:, 1:], ref, rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("B", [120, 131])
+def test_dense_patch_embed_persistent(gpu, B):
+    """The model's bf16 patch GEMM at a batch that takes the persistent kernel (EPI_POS with the
+    bf16 position table in resid): + bias + pos[t+1], rows remapped past the CLS rows, statistics
+    of the stored rows; CLS rows and their statistics untouched. B = 131: an M edge mid-image."""
+    P, K, N = 196, 768, 768
+    A64, W64, b64 = _rand((B * P, K), 15), _rand((K, N), 16, 1 / 28.0), _rand((N,), 17, 0.1)
+    pos64 = _rand((P + 1, N), 18, 0.05)
+    A = A64.to(torch.bfloat16).to(gpu)
+    wp, kpad, npad = _ops.pack(W64.float().to(gpu), "bf16")
+    bias = torch.zeros(npad, device=gpu)
+    bias[:N] = b64.float().to(gpu)
+    pos = pos64.float().to(gpu)
+    pos_h = pos.to(torch.bfloat16)
+    C = torch.full((B * (P + 1), N), 7.0, dtype=torch.bfloat16, device=gpu)
+    st = torch.full((B * (P + 1), _nslots(N), 2), float("nan"), device=gpu)
+    _ops.dense("bf16", _lib.EPI_BIAS | _lib.EPI_POS | _lib.EPI_STATS, A, wp, kpad, npad, B * P, N,
+               bias=bias, pos=pos, P=P, C=C, resid=pos_h, stats_out=st, ln_width=N)
+    torch.cuda.synchronize()
+    ref = (_q(A64, "bf16") @ _q(W64.float().double(), "bf16") + b64.float().double()).reshape(B, P, N)
+    ref = ref + _q(pos64.float().double(), "bf16")[1:]
+    got = C.double().cpu().reshape(B, P + 1, N)
+    assert torch.all(got[:, 0] == 7.0), "CLS rows must be left untouched by the patch GEMM"
+    torch.testing.assert_close(got[:, 1:], ref, rtol=2e-2, atol=2e-2)
+    stc = st.cpu().reshape(B, P + 1, -1, 2)
+    assert torch.isnan(stc[:, 0]).all(), "CLS-row statistics must be left untouched"
+    rows = got[:, 1:].reshape(B * P, N)
+    torch.testing.assert_close(stc[:, 1:].double().sum(2).reshape(B * P, 2), _stats32(rows).double().sum(1),
+                               rtol=1e-4, atol=1e-2)
+
+
 def _attn_ref(qkv64, B, N, H):
     q, k, v = qkv64.reshape(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
     s = torch.einsum("bhid,bhjd->bhij", q, k) * 0.125
