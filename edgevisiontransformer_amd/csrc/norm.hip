@@ -12,6 +12,8 @@
 // vectors of that row coalesced in (p1 p2 c) order. The first strip of each image also writes the
 // CLS token row x[b, 0] = cls + pos[0] (reference vit.py:48-51) into the token stream, with the
 // row statistics the folded LayerNorm of layer 0 needs.
+#include <type_traits>
+
 #include "common.h"
 #include "evt_internal.h"
 
@@ -156,8 +158,14 @@ __global__ __launch_bounds__(256) void patchify_cm_kernel(const float* __restric
     const float* sp = strip + c * per_c + p1 * HW + ww * ps + p2;
     const f32x4 v0 = *(const f32x4*)sp, v1 = *(const f32x4*)(sp + 4);
     TO* op = orow + (int64_t)ww * pd + q * 8;
-    store4(op, v0);
-    store4(op + 4, v1);
+    if constexpr (std::is_same<TO, bf16>::value) {  // one 16-B store per 8 pixels
+      const bf16x8 o = {(bf16)v0[0], (bf16)v0[1], (bf16)v0[2], (bf16)v0[3],
+                        (bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
+      *(bf16x8*)op = o;
+    } else {
+      store4(op, v0);
+      store4(op + 4, v1);
+    }
   }
   if (hh == 0 && tid < 64) {  // one wave writes the CLS row and its LayerNorm statistics
     const int64_t row = (int64_t)b * (np * np + 1);
