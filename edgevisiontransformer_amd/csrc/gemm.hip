@@ -1152,6 +1152,18 @@ __device__ __forceinline__ int pos_img(int m, int P) {
 }
 __device__ __forceinline__ int pos_orow(int m, int P) { return m + pos_img(m, P) + 1; }
 
+// A store of more than 64 bits reads its data VGPRs after issue: a vector instruction that
+// overwrites them in the very next slot can land first (measured: the row-statistics code's
+// v_and_b32 v3 right after buffer_store_dwordx4 v[2:5] stored zeros into dword 1 of 8 lanes in
+// about 1 launch in 12). hipcc 7.2 inserts no wait state there for gfx950; this fence keeps one
+// instruction between every such store and whatever the scheduler would put next
+// (scripts/probe/store_hazard.py checks the assembly).
+__device__ __forceinline__ void wide_store_fence() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 0");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // Epilogue of one 256 x 256 tile straight from the accumulators (VALU-bound: every instruction
 // here is paid with the MFMA pipe idle, so the arithmetic is in packed form throughout):
 //   LNIN   r (acc - mu colsum) + c      2 v_pk_fma per column pair
@@ -1380,6 +1392,7 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
         }
         if (keep)  // nontemporal (aux nt): whole lines streamed past L2
           __builtin_amdgcn_raw_buffer_store_b128(v, cs, svo, so, 2);
+        wide_store_fence();
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }

@@ -26,22 +26,29 @@ rst = _stats(x)
 ref = A.float() @ W.bfloat16().float() + b + _ln(x.float(), g, be)
 lib = _lib.load_library()
 flags = EPI.EPI_BIAS | EPI.EPI_RESID | EPI.EPI_RESLN | EPI.EPI_STATS
-for variant, reps in [(0, int(sys.argv[1]) if len(sys.argv) > 1 else 12), (16, 4)]:
+def launch(variant, tag):
     lib.evt_set_gemm_variant(variant)
-    for r in range(reps):
-        so = torch.full((M, S, 2), float("nan"), device=A.device)
-        C = torch.full((M, D), float("nan"), device=A.device).bfloat16()
-        C = _ops.dense("bf16", flags, A, wp, kpad, npad, M, D, bias=bias, resid=x, rstats=rst,
-                       rgamma=g, rbeta=be, stats_out=so, ln_width=D, C=C)
-        torch.cuda.synchronize()
-        bad = ~torch.isclose(C.float(), ref, rtol=2e-2, atol=2e-2)
-        n = int(bad.sum())
-        msg = f"variant {variant} rep {r}: {n} bad"
-        if n:
-            idx = bad.nonzero()
-            rows = sorted(set(idx[:, 0].tolist()))
-            cols = sorted(set(idx[:, 1].tolist()))
-            msg += f" rows {rows[:12]} ({len(rows)}) cols {cols[:12]}..{cols[-4:]} ({len(cols)})"
-            msg += f" nan {int(torch.isnan(C.float()[bad]).sum())}"
-        print(msg, flush=True)
+    so = torch.full((M, S, 2), float("nan"), device=A.device)
+    C = torch.zeros((M, D), device=A.device).bfloat16()
+    C = _ops.dense("bf16", flags, A, wp, kpad, npad, M, D, bias=bias, resid=x, rstats=rst,
+                   rgamma=g, rbeta=be, stats_out=so, ln_width=D, C=C)
+    torch.cuda.synchronize()
+    bad = ~torch.isclose(C.float(), ref, rtol=2e-2, atol=2e-2)
+    n = int(bad.sum())
+    if n:
+        idx = bad.nonzero()
+        rows = sorted(set(idx[:, 0].tolist()))
+        cols = sorted(set(idx[:, 1].tolist()))
+        print(f"{tag}: {n} bad rows {rows[:8]} ({len(rows)}) cols {cols[:8]} ({len(cols)}) "
+              f"zero {int((C.float()[bad] == 0).sum())}", flush=True)
+    return n
+
+
+# the GPU test's order (stream-K twice, then the persistent kernel), repeated
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 12
+tot = {16: 0, 0: 0}
+for r in range(reps):
+    for v, tag in ((16, "sk"), (16, "sk2"), (0, "pers")):
+        tot[v] += launch(v, f"rep {r} {tag}") > 0
+print("launches with errors: stream-K", tot[16], "of", 2 * reps, "; persistent", tot[0], "of", reps)
 lib.evt_set_gemm_variant(0)
