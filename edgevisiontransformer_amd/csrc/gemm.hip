@@ -687,11 +687,14 @@ struct NoOp {
 
 // pre1: run by wave group 1 in the slot where it waits one barrier for group 0 (per-tile LDS
 // setup work that is then off the critical path); mid: after K-tile 0 (nk >= 3 only).
-template <int X, bool OPEN = false, typename Pre1 = NoOp, typename Mid = NoOp>
+// last: issues LX further VMEM loads per wave just before the last K-tile (added to its waits:
+// they are younger than every DMA that tile waits for).
+template <int X, bool OPEN = false, typename Pre1 = NoOp, typename Mid = NoOp, int LX = 0,
+          typename Last = NoOp>
 __device__ __forceinline__ void big8_loop(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
                                           int wave, int lane, int wm, int wn, int m0, int n0,
                                           int nk, bool cont = false, int nm0 = 0, int nn0 = 0,
-                                          Pre1 pre1 = {}, Mid mid = {}) {
+                                          Pre1 pre1 = {}, Mid mid = {}, Last last = {}) {
   if (nk >= 2) wait_vm<8 + X>();
   else wait_vm<4 + X>();
   big8_bar();
@@ -705,12 +708,15 @@ __device__ __forceinline__ void big8_loop(const GemmParams& p, char* smem, f32x4
     int t = 1;
     for (; t + 2 < nk; ++t) big8_ktile<0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t);
     big8_ktile<1, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, cont, nm0, nn0);
-    big8_ktile<2, 0, OPEN>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1, cont, nm0, nn0);
+    last();
+    big8_ktile<2, LX, OPEN>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1, cont, nm0, nn0);
   } else if (nk == 2) {
     big8_ktile<1, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, cont, nm0, nn0);
-    big8_ktile<2, 0, OPEN>(p, smem, acc, wave, lane, wm, wn, m0, n0, 1, cont, nm0, nn0);
+    last();
+    big8_ktile<2, LX, OPEN>(p, smem, acc, wave, lane, wm, wn, m0, n0, 1, cont, nm0, nn0);
   } else {
-    big8_ktile<2, X, OPEN>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0);
+    last();
+    big8_ktile<2, X + LX, OPEN>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0);
   }
   if (!OPEN && wm == 0) big8_bar();
 }
@@ -1173,10 +1179,30 @@ __device__ __forceinline__ void wide_store_fence() {
 // Residual loads and output stores go through tile buffer resources (SGPR base per tile, lane
 // offsets tile-invariant, row offsets in SGPRs): no per-store 64-bit address arithmetic and no
 // exec-mask branches for the M edge.
-template <int FL, int DBG = 0, bool PADN = true>
+// Residual of the first ER row pairs (the epilogue's rr[0 .. ER-1]), issued before the tile's last
+// K-tile so that part of the residual fetch is in flight under its MFMAs (ER = 1: the most that
+// fits in 256 VGPRs without spilling).
+template <int ER>
+__device__ __forceinline__ void pers_resid_early(const GemmParams& p, int wm, int wn, int lane,
+                                                 int m0, int n0, u32x4 (&rre)[2][4]) {
+  const int frow = lane & 15, fg = lane >> 4;
+  const int rl = wm * 128 + (fg & 1) * 16 + frow, cl = wn * 64 + (fg >> 1) * 8;
+  const __amdgpu_buffer_rsrc_t rs = tile_rsrc(p.resid, p.ldr, p.M, m0, n0);
+  const int vo = (rl * (int)p.ldr + cl) * 2;
+#pragma unroll
+  for (int k = 0; k < ER; ++k) {
+    const int so = __builtin_amdgcn_readfirstlane(32 * k * (int)p.ldr * 2);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+      rre[k][nt] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 32 * nt, so, 0));
+  }
+}
+
+template <int FL, int DBG = 0, bool PADN = true, int ER = 0>
 __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
                                               int wave, int wm, int wn, int m0, int n0, int tn,
-                                              int lane, bool interior, int iter = 0) {
+                                              int lane, bool interior, int iter = 0,
+                                              const u32x4 (*rre)[4] = nullptr) {
   // DBG 3: sub-stamps 3..5 of the tile's timeline row (wave 0, lane 0)
   auto stamp = [&](int k) {
     if (DBG == 3 && wave == 0 && lane == 0 && iter < 16)
@@ -1276,7 +1302,8 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
       const int so = __builtin_amdgcn_readfirstlane(32 * k * (int)p.ldr * 2);
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
-        rr[k][nt] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 32 * nt, so, 0));
+        rr[k][nt] = k < ER ? rre[k][nt]
+                           : __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 32 * nt, so, 0));
     }
   } else if constexpr ((FL & EPI_POS) != 0) {  // pos[t + 1][n0 + cl + 16 nt ..] (bf16 table)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -1427,6 +1454,8 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
 
 template <int FL, int DBG = 0, bool PADN = true>
 __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int total) {
+  // a quarter of the residual before the last K-tile (out-proj 160 -> 153 us); DBG 20: A/B without
+  constexpr int ER = ((FL & EPI_RESID) != 0 && DBG != 7 && DBG != 20 && DBG != 18) ? 1 : 0;
   __shared__ __attribute__((aligned(16))) char smem[PERS_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1460,6 +1489,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
       for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     int ln = lane;
     asm volatile("" : "+v"(ln));  // per-tile lane addresses: not hoisted out of the tile loop
+    u32x4 rre[2][4];  // ER: residual row pair 0 loaded before the last K-tile
     const int next = tile + G;
     const bool has_next = next < total;
     int ntm = 0, ntn = 0;
@@ -1469,6 +1499,9 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
     }
     // even nk: the next tile's prologue rides in the last K-tiles' idle DMA slots (big8_ktile)
     const bool cont = has_next && !(nk & 1) && DBG != 16;
+    auto last = [&]() {
+      if constexpr (ER > 0) pers_resid_early<ER>(p, wm, wn, ln, m0, n0, rre);
+    };
     if (early) {
       // this tile's LayerNorm coefficients by wave group 1 while it waits for group 0's first
       // phase; the next tile's statistics rows / column vectors DMA'd after K-tile 0 (PERS_RAW is
@@ -1481,12 +1514,14 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
         big8_loop<PERS_X>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
                           ntn * BIG_BN, pre1, mid);
       else
-        big8_loop<PERS_X, true>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
-                                ntn * BIG_BN, pre1, mid);
+        big8_loop<PERS_X, true, decltype(pre1), decltype(mid), ER * 4, decltype(last)>(
+            p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM, ntn * BIG_BN, pre1,
+            mid, last);
       stamp(1);
       if (has_next && !cont) big8_prologue(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nk);
     } else {
-      big8_loop<PERS_X>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM, ntn * BIG_BN);
+      big8_loop<PERS_X, false, NoOp, NoOp, ER * 4, decltype(last)>(
+          p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM, ntn * BIG_BN, {}, {}, last);
       stamp(1);
       pers_coef<FL>(p, smem, tid);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1503,7 +1538,8 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
     if constexpr (DBG == 6)  // A/B: the round-1 epilogue
       pers_epilogue_v1<FL, 0, PADN>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior);
     else
-      pers_epilogue<FL, DBG, PADN>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior, iter);
+      pers_epilogue<FL, DBG, PADN, ER>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior, iter,
+                                       rre);
     stamp(7);
     ++iter;
     if (!has_next) break;
@@ -1703,7 +1739,7 @@ constexpr bool pers_fl(int fl) {
 
 // persistent kernel: supported epilogue, 8-column output groups, LN rows of <= 8 slots
 bool use_pers(const GemmParams& p, int flags) {
-  if (g_gemm_variant != 0 && (g_gemm_variant < 9 || g_gemm_variant > 23 || g_gemm_variant == 12 ||
+  if (g_gemm_variant != 0 && (g_gemm_variant < 9 || g_gemm_variant > 24 || g_gemm_variant == 12 ||
                               g_gemm_variant == 14))
     return false;
   if (p.N % 8 || p.vec_ok < 2) return false;
@@ -1738,6 +1774,8 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 17, false>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 21)  // A/B: next-tile prologue issued after the main loop
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 16, false>), dim3(G), dim3(512), 0, s, q, total);
+  else if (g_gemm_variant == 24)  // A/B: the whole residual loaded in the epilogue
+    hipLaunchKernelGGL((gemm_pers_kernel<FL, 20, false>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 20)  // ablation: no residual loads (out-proj 153 -> 115 us)
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 7, false>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 18)  // ablation: epilogue without the GELU
