@@ -13,7 +13,7 @@ grep smoke $O/smoke.log
 timeout -k 10 600 python bench.py > $O/bench.log 2>&1 || exit 1
 tail -1 $O/bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['model_roofline'], d['roofline']['achieved'], d['roofline']['frac'], d['roofline']['per_role_us'], d['cpu_baseline']['value'])"
 TAG=r2v5_bench BENCH_ARGS="--cpu-seconds 0" STEPS=10 bash scripts/gpu_prof.sh > /dev/null 2>&1 || exit 1
-tail -1 gpurun_out/prof_r2v5_bench/bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('under rocprof: fc1', d['roofline']['avg_launch_us'])"
+grep '^{' gpurun_out/prof_r2v5_bench/bench.log | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('under rocprof: fc1', d['roofline']['avg_launch_us'])"
 python scripts/kstats.py gpurun_out/prof_r2v5_bench/kernel_stats.csv 512 > $O/kstats.txt; head -10 $O/kstats.txt
 bash scripts/gpu_pmc_fc1.sh > $O/pmc.log 2>&1 || exit 1
 tail -3 $O/pmc.log
