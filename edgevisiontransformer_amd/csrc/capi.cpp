@@ -1334,7 +1334,7 @@ int evt_set_fusion(int flags) {
 
 int evt_set_gemm_variant(int variant) {
   if (variant != 0 && variant != 1 && variant != 2 && variant != 6 && variant != 8 &&
-      !(variant >= 9 && variant <= 24) && variant != 106 && variant != 108)
+      !(variant >= 9 && variant <= 25) && variant != 106 && variant != 108)
     return fail(EVT_EINVAL, "variant must be 0, 1, 2, 6, 8, 9-23, 106 or 108");
   gemm_set_variant(variant);
   return EVT_OK;

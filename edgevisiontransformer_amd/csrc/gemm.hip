@@ -550,6 +550,10 @@ __device__ __forceinline__ void big_epilogue(const GemmParams& p, char* smem, f3
 // while one group issues MFMAs (at raised priority) the other issues ds_reads and DMAs on the
 // same SIMD (waves w and w + 4 share a SIMD).
 // ---------------------------------------------------------------------------------------------
+struct NoOp {
+  __device__ void operator()() const {}
+};
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -607,10 +611,12 @@ __device__ __forceinline__ void big8_prologue(const GemmParams& p, char* smem, i
 // OPEN (last K-tile of a persistent-kernel tile): wave group 1 skips the barrier that closes its
 // final MFMA phase and group 0 the resync barrier after the loop, so group 0 starts its epilogue
 // while group 1 still issues its last 16 MFMAs (the two barriers cancel in every wave's count).
-template <int MODE, int X, bool OPEN = false>
+// ph3: issues X3 further VMEM loads at the start of phase 3 (added to that phase's wait).
+template <int MODE, int X, bool OPEN = false, int X3 = 0, typename Ph3 = NoOp>
 __device__ __forceinline__ void big8_ktile(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
                                            int wave, int lane, int wm, int wn, int m0, int n0,
-                                           int t, bool cont = false, int nm0 = 0, int nn0 = 0) {
+                                           int t, bool cont = false, int nm0 = 0, int nn0 = 0,
+                                           Ph3 ph3 = {}) {
   const int frow = lane & 15, fsw = lane & 7, fg = lane >> 4;
   const EVT_LDS char* As = (const EVT_LDS char*)smem + (t & 1) * BIG_STAGE;
   const EVT_LDS char* Ws = As + BIG_TILE;
@@ -640,6 +646,7 @@ __device__ __forceinline__ void big8_ktile(const GemmParams& p, char* smem, f32x
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) af[mt][ks] = rd(As, wm * 128 + 64 + mt * 16 + frow, ks);
     }
+    if (ph == 3) ph3();
     // DMA of region s = 4 t + ph + 6
     if (MODE == 0 || (MODE == 1 && ph < 2)) {
       if (ph < 2) big8_stage(p, smem, wave, lane, m0, n0, t + 1, ph + 2);
@@ -652,7 +659,8 @@ __device__ __forceinline__ void big8_ktile(const GemmParams& p, char* smem, f32x
     if (ph != 2) {
       if (MODE == 0) wait_vm<8 + X>();
       else if (cont) {  // the steady-state DMA pattern continues: steady-state waits
-        wait_vm<8 + X>();
+        if (ph == 3) wait_vm<8 + X + X3>();
+        else wait_vm<8 + X>();
       } else if (MODE == 1) {
         if (ph == 3) wait_vm<4 + X>();
         else wait_vm<8 + X>();
@@ -681,20 +689,18 @@ __device__ __forceinline__ void big8_ktile(const GemmParams& p, char* smem, f32x
 
 // Main loop over the nk K-tiles after big8_prologue (whose DMAs may be followed by X further
 // VMEM instructions per wave, or by a vmcnt(0)). Ends with every wave past a common barrier.
-struct NoOp {
-  __device__ void operator()() const {}
-};
 
 // pre1: run by wave group 1 in the slot where it waits one barrier for group 0 (per-tile LDS
 // setup work that is then off the critical path); mid: after K-tile 0 (nk >= 3 only).
 // last: issues LX further VMEM loads per wave just before the last K-tile (added to its waits:
 // they are younger than every DMA that tile waits for).
 template <int X, bool OPEN = false, typename Pre1 = NoOp, typename Mid = NoOp, int LX = 0,
-          typename Last = NoOp>
+          typename Last = NoOp, int LX3 = 0, typename Last3 = NoOp>
 __device__ __forceinline__ void big8_loop(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
                                           int wave, int lane, int wm, int wn, int m0, int n0,
                                           int nk, bool cont = false, int nm0 = 0, int nn0 = 0,
-                                          Pre1 pre1 = {}, Mid mid = {}, Last last = {}) {
+                                          Pre1 pre1 = {}, Mid mid = {}, Last last = {},
+                                          Last3 last3 = {}) {
   if (nk >= 2) wait_vm<8 + X>();
   else wait_vm<4 + X>();
   big8_bar();
@@ -709,14 +715,17 @@ __device__ __forceinline__ void big8_loop(const GemmParams& p, char* smem, f32x4
     for (; t + 2 < nk; ++t) big8_ktile<0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t);
     big8_ktile<1, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, cont, nm0, nn0);
     last();
-    big8_ktile<2, LX, OPEN>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1, cont, nm0, nn0);
+    big8_ktile<2, LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1, cont, nm0, nn0,
+                                 last3);
   } else if (nk == 2) {
     big8_ktile<1, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, cont, nm0, nn0);
     last();
-    big8_ktile<2, LX, OPEN>(p, smem, acc, wave, lane, wm, wn, m0, n0, 1, cont, nm0, nn0);
+    big8_ktile<2, LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, 1, cont, nm0, nn0,
+                                 last3);
   } else {
     last();
-    big8_ktile<2, X + LX, OPEN>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0);
+    big8_ktile<2, X + LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, false, 0, 0,
+                                     last3);
   }
   if (!OPEN && wm == 0) big8_bar();
 }
@@ -1182,7 +1191,7 @@ __device__ __forceinline__ void wide_store_fence() {
 // Residual of the first ER row pairs (the epilogue's rr[0 .. ER-1]), issued before the tile's last
 // K-tile so that part of the residual fetch is in flight under its MFMAs (ER = 1: the most that
 // fits in 256 VGPRs without spilling).
-template <int ER>
+template <int K0, int K1>
 __device__ __forceinline__ void pers_resid_early(const GemmParams& p, int wm, int wn, int lane,
                                                  int m0, int n0, u32x4 (&rre)[2][4]) {
   const int frow = lane & 15, fg = lane >> 4;
@@ -1190,7 +1199,7 @@ __device__ __forceinline__ void pers_resid_early(const GemmParams& p, int wm, in
   const __amdgpu_buffer_rsrc_t rs = tile_rsrc(p.resid, p.ldr, p.M, m0, n0);
   const int vo = (rl * (int)p.ldr + cl) * 2;
 #pragma unroll
-  for (int k = 0; k < ER; ++k) {
+  for (int k = K0; k < K1; ++k) {
     const int so = __builtin_amdgcn_readfirstlane(32 * k * (int)p.ldr * 2);
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
@@ -1455,7 +1464,8 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
 template <int FL, int DBG = 0, bool PADN = true>
 __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int total) {
   // a quarter of the residual before the last K-tile (out-proj 160 -> 153 us); DBG 20: A/B without
-  constexpr int ER = ((FL & EPI_RESID) != 0 && DBG != 7 && DBG != 20 && DBG != 18) ? 1 : 0;
+  constexpr int ER = ((FL & EPI_RESID) != 0 && DBG != 7 && DBG != 20 && DBG != 18)
+                         ? (DBG == 21 ? 1 : 2) : 0;  // DBG 21: A/B with one quarter
   __shared__ __attribute__((aligned(16))) char smem[PERS_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1500,7 +1510,10 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
     // even nk: the next tile's prologue rides in the last K-tiles' idle DMA slots (big8_ktile)
     const bool cont = has_next && !(nk & 1) && DBG != 16;
     auto last = [&]() {
-      if constexpr (ER > 0) pers_resid_early<ER>(p, wm, wn, ln, m0, n0, rre);
+      if constexpr (ER > 0) pers_resid_early<0, 1>(p, wm, wn, ln, m0, n0, rre);
+    };
+    auto last3 = [&]() {  // row pair 1 once the n-half-1 fragments are dead (phase 3)
+      if constexpr (ER > 1) pers_resid_early<1, 2>(p, wm, wn, ln, m0, n0, rre);
     };
     if (early) {
       // this tile's LayerNorm coefficients by wave group 1 while it waits for group 0's first
@@ -1514,14 +1527,16 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
         big8_loop<PERS_X>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
                           ntn * BIG_BN, pre1, mid);
       else
-        big8_loop<PERS_X, true, decltype(pre1), decltype(mid), ER * 4, decltype(last)>(
-            p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM, ntn * BIG_BN, pre1,
-            mid, last);
+        big8_loop<PERS_X, true, decltype(pre1), decltype(mid), (ER > 0 ? 4 : 0), decltype(last),
+                  (ER > 1 ? 4 : 0), decltype(last3)>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont,
+                                                   ntm * BIG_BM, ntn * BIG_BN, pre1, mid, last,
+                                                   last3);
       stamp(1);
       if (has_next && !cont) big8_prologue(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nk);
     } else {
-      big8_loop<PERS_X, false, NoOp, NoOp, ER * 4, decltype(last)>(
-          p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM, ntn * BIG_BN, {}, {}, last);
+      big8_loop<PERS_X, false, NoOp, NoOp, (ER > 0 ? 4 : 0), decltype(last), (ER > 1 ? 4 : 0),
+                decltype(last3)>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
+                                 ntn * BIG_BN, {}, {}, last, last3);
       stamp(1);
       pers_coef<FL>(p, smem, tid);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1739,7 +1754,7 @@ constexpr bool pers_fl(int fl) {
 
 // persistent kernel: supported epilogue, 8-column output groups, LN rows of <= 8 slots
 bool use_pers(const GemmParams& p, int flags) {
-  if (g_gemm_variant != 0 && (g_gemm_variant < 9 || g_gemm_variant > 24 || g_gemm_variant == 12 ||
+  if (g_gemm_variant != 0 && (g_gemm_variant < 9 || g_gemm_variant > 25 || g_gemm_variant == 12 ||
                               g_gemm_variant == 14))
     return false;
   if (p.N % 8 || p.vec_ok < 2) return false;
@@ -1776,6 +1791,8 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 16, false>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 24)  // A/B: the whole residual loaded in the epilogue
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 20, false>), dim3(G), dim3(512), 0, s, q, total);
+  else if (g_gemm_variant == 25)  // A/B: one residual quarter early (not two)
+    hipLaunchKernelGGL((gemm_pers_kernel<FL, 21, false>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 20)  // ablation: no residual loads (out-proj 153 -> 115 us)
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 7, false>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 18)  // ablation: epilogue without the GELU
