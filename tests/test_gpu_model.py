@@ -3,8 +3,8 @@ the reference's own torch_layers, tests/golden/make_golden.py) and the numpy ora
 
 Tolerances (stated):
   * f32 path (exact fp32 MFMA): max |logits - golden| <= 1e-3.
-  * bf16 path (bf16 operands, fp32 accumulate / LN / softmax / GELU): max-abs <= 5e-2 and
-    per-row cosine >= 0.999 vs the fp64 golden.
+  * bf16 path (bf16 operands, fp32 accumulate / LN / softmax / GELU): max-abs <= 3e-2 and
+    per-row cosine >= 0.9995 vs the fp64 golden.
 """
 import os
 
@@ -20,7 +20,7 @@ from tests.golden.make_golden import CASES, case_config
 pytestmark = pytest.mark.gpu
 
 F32_TOL = 1e-3
-BF16_ABS, BF16_COS = 5e-2, 0.999
+BF16_ABS, BF16_COS = 3e-2, 0.9995
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 

@@ -2,8 +2,8 @@
 (tests/golden/make_golden_swin.py, pinned by the numpy oracle), and the window-attention and
 patch-merge kernels against the oracle on identical rounded inputs.
 
-Tolerances: f32 path max-abs <= 1e-3 on logits; bf16 path max-abs <= 5e-2 and per-row cosine
->= 0.999 (as for DeiT). Kernel tests: f32 within 2e-5, bf16 within 3e-2 (bf16
+Tolerances: f32 path max-abs <= 1e-3 on logits; bf16 path max-abs <= 3e-2 and per-row cosine
+>= 0.9995 (as for DeiT). Kernel tests: f32 within 2e-5, bf16 within 3e-2 (bf16
 output rounding of O ~ 4e-3 relative plus bf16 P) of the fp64 restatement.
 """
 import ctypes
@@ -44,8 +44,8 @@ def test_swin_golden(gpu, name, dtype):
     if dtype == "f32":
         assert err <= 1e-3, f"{name} f32 max-abs {err:.3e}"
     else:
-        assert err <= 5e-2, f"{name} bf16 max-abs {err:.3e}"
-        assert _cos_rows(out, z["logits"]).min() >= 0.999
+        assert err <= 3e-2, f"{name} bf16 max-abs {err:.3e}"
+        assert _cos_rows(out, z["logits"]).min() >= 0.9995
 
 
 def test_swin_batch_independence_and_graph(gpu):
@@ -152,4 +152,4 @@ def test_fused_stage1_mlp_matches_gemm_path(gpu):
         _lib.check(lib.evt_set_gemm_variant(0))
     ref = swin_ref.swin_forward(params, cfg, make_images(6, seed=16, image_size=56))
     assert np.abs(fused - gemm).max() <= 3e-2
-    assert np.abs(fused - ref).max() <= 5e-2 and _cos_rows(fused, ref).min() >= 0.999
+    assert np.abs(fused - ref).max() <= 3e-2 and _cos_rows(fused, ref).min() >= 0.9995

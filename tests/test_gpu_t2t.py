@@ -3,7 +3,7 @@ against the numpy oracle (oracle/t2t_ref.py) and the golden fixtures.
 
 Tolerances (stated): unfold is a copy, exact in both dtypes (bf16: the same round-to-nearest of
 the same inputs); performer core f32 <= 2e-4 relative to the output scale, bf16 <= 3e-2;
-model logits f32 <= 1e-3 max-abs, bf16 <= 5e-2 max-abs and row cosine >= 0.999.
+model logits f32 <= 1e-3 max-abs, bf16 <= 3e-2 max-abs and row cosine >= 0.9995.
 The T2T stage itself is "parity unpinned" (no runnable reference): the oracle is a
 restatement of the reference lines; the encoder part is pinned by the reference torch twins.
 """
@@ -143,7 +143,7 @@ def test_t2t_golden_bf16(gpu, name):
     ref = z["logits"]
     err = np.abs(out - ref).max()
     cos = ((out * ref).sum(1) / (np.linalg.norm(out, axis=1) * np.linalg.norm(ref, axis=1))).min()
-    assert err <= 5e-2 and cos >= 0.999, f"{name}: bf16 max-abs {err:.3e} cos {cos:.5f}"
+    assert err <= 3e-2 and cos >= 0.9995, f"{name}: bf16 max-abs {err:.3e} cos {cos:.5f}"
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f32"])

@@ -1,6 +1,6 @@
 """STANDARD DeiT / ViT semantics (EVT_VIT_STANDARD): oracle vs the HF-produced fp64 goldens (CPU),
 checkpoint mapping round trips (CPU), and the HIP path vs the goldens (GPU; f32 max-abs <= 1e-3,
-bf16 max-abs <= 5e-2 and per-row cosine >= 0.999)."""
+bf16 max-abs <= 3e-2 and per-row cosine >= 0.9995)."""
 import os
 
 import numpy as np
@@ -67,5 +67,5 @@ def test_std_vit_gpu(gpu, name, dtype):
     if dtype == "f32":
         assert err <= 1e-3, err
     else:
-        assert err <= 5e-2, err
-        assert _cos_rows(out, z["logits"]).min() >= 0.999
+        assert err <= 3e-2, err
+        assert _cos_rows(out, z["logits"]).min() >= 0.9995
