@@ -207,8 +207,8 @@ __device__ __forceinline__ void attn_tile_bf16(const AttnParams& p, const EVT_LD
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) {
       const u32x4 v = {x0[pr], x1[pr], y0[pr], y1[pr]};
-      if (PLAIN_STORE) *(u32x4*)(op + 32 * pr) = v;
-      else __builtin_nontemporal_store(v, (u32x4*)(op + 32 * pr));
+      if (PLAIN_STORE) store_b128(op + 32 * pr, v);
+      else store_b128_nt(op + 32 * pr, v);
     }
   }
 }

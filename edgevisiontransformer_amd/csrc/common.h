@@ -32,7 +32,46 @@ __device__ __forceinline__ f32x4 load4(const bf16* p) {
   bf16x4 v = *(const bf16x4*)p;
   return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
 }
-__device__ __forceinline__ void store4(float* p, f32x4 v) { *(f32x4*)p = v; }
+// ---- wide (> 64-bit) vector-memory stores -------------------------------------------------
+// A store of more than 64 bits reads its data VGPRs after issue: a VALU write to them fewer than
+// 2 wait states later (gfx940 family, gfx950 included) can land first. hipcc 7.2 inserts those
+// wait states for global / flat stores but not for buffer stores with an SGPR soffset, and in the
+// persistent GEMM epilogue a v_and_b32 v3 right after buffer_store_dwordx4 v[2:5] stored zeros into
+// dword 1 of 8 lanes in about 1 launch in 12. EVERY store of more than 64 bits in this library goes
+// through the helpers below, each followed by wide_store_fence(): a scheduling barrier and s_nop 1
+// (2 wait states) between the store and whatever the scheduler would put next.
+// tests/test_isa_hazards.py checks the built code objects (every wide vector-memory store is
+// fenced, no VALU write of its data VGPRs inside 2 wait states) and that no kernel source issues
+// such a store except through these helpers.
+__device__ __forceinline__ void wide_store_fence() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 1");
+  __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void store_b128(void* p, u32x4 v) {
+  *(u32x4*)p = v;
+  wide_store_fence();
+}
+// non-temporal (streaming past L2)
+__device__ __forceinline__ void store_b128_nt(void* p, u32x4 v) {
+  __builtin_nontemporal_store(v, (u32x4*)p);
+  wide_store_fence();
+}
+// AUX: the cache-policy bits (2 = nt)
+template <int AUX>
+__device__ __forceinline__ void buffer_store_b128(u32x4 v, __amdgpu_buffer_rsrc_t rs, int voff,
+                                                  int soff) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, AUX);
+  wide_store_fence();
+}
+__device__ __forceinline__ void store_f32x4(float* p, f32x4 v) {
+  store_b128(p, __builtin_bit_cast(u32x4, v));
+}
+__device__ __forceinline__ void store_bf16x8(bf16* p, bf16x8 v) {
+  store_b128(p, __builtin_bit_cast(u32x4, v));
+}
+
+__device__ __forceinline__ void store4(float* p, f32x4 v) { store_f32x4(p, v); }
 __device__ __forceinline__ void store4(bf16* p, f32x4 v) {
   bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
   *(bf16x4*)p = o;
@@ -49,7 +88,9 @@ __device__ __forceinline__ void permlane16_swap(unsigned& x, unsigned& y) {
 
 // Non-temporal (streaming) stores for GEMM outputs: they go to HBM without displacing the operand
 // panels the other CUs of the XCD still read from L2 (measured: -15% on the K = 768 GEMMs).
-__device__ __forceinline__ void store4_nt(float* p, f32x4 v) { __builtin_nontemporal_store(v, (f32x4*)p); }
+__device__ __forceinline__ void store4_nt(float* p, f32x4 v) {
+  store_b128_nt(p, __builtin_bit_cast(u32x4, v));
+}
 __device__ __forceinline__ void store4_nt(bf16* p, f32x4 v) {
   const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
   __builtin_nontemporal_store(o, (bf16x4*)p);

@@ -328,7 +328,7 @@ __device__ __forceinline__ void epi_rows8_t(const GemmParams& p, EVT_LDS char* s
                       (bf16)v[1][0], (bf16)v[1][1], (bf16)v[1][2], (bf16)v[1][3]};
     if (ok) {
       bf16* cp = (bf16*)p.C + orow * p.ldc + n;
-      if (full) __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), (u32x4*)cp);
+      if (full) store_b128_nt(cp, __builtin_bit_cast(u32x4, o));
       else
 #pragma unroll
         for (int j = 0; j < 8; ++j)
@@ -1113,7 +1113,7 @@ __device__ __forceinline__ void pers_epilogue_v1(const GemmParams& p, char* smem
         }
         if ((interior || m < p.M) && rcol_ok && keep) {
           u32x4* cp = (u32x4*)((bf16*)p.C + (int64_t)m * p.ldc + n0 + wn * 64 + rch * 8);
-          __builtin_nontemporal_store(v, cp);  // whole lines: streamed past L2
+          store_b128_nt(cp, v);  // whole lines: streamed past L2
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1166,18 +1166,6 @@ __device__ __forceinline__ int pos_img(int m, int P) {
   return (int)(((float)m + 0.5f) * (1.0f / (float)P));
 }
 __device__ __forceinline__ int pos_orow(int m, int P) { return m + pos_img(m, P) + 1; }
-
-// A store of more than 64 bits reads its data VGPRs after issue: a vector instruction that
-// overwrites them in the very next slot can land first (measured: the row-statistics code's
-// v_and_b32 v3 right after buffer_store_dwordx4 v[2:5] stored zeros into dword 1 of 8 lanes in
-// about 1 launch in 12). hipcc 7.2 inserts no wait state there for gfx950; this fence keeps one
-// instruction between every such store and whatever the scheduler would put next
-// (scripts/probe/store_hazard.py checks the assembly).
-__device__ __forceinline__ void wide_store_fence() {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_nop 0");
-  __builtin_amdgcn_sched_barrier(0);
-}
 
 // Epilogue of one 256 x 256 tile straight from the accumulators (VALU-bound: every instruction
 // here is paid with the MFMA pipe idle, so the arithmetic is in packed form throughout):
@@ -1427,8 +1415,7 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
                  wn * 64 + rch * 8) * 2;
         }
         if (keep)  // nontemporal (aux nt): whole lines streamed past L2
-          __builtin_amdgcn_raw_buffer_store_b128(v, cs, svo, so, 2);
-        wide_store_fence();
+          buffer_store_b128<2>(v, cs, svo, so);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
@@ -1670,8 +1657,8 @@ __global__ __launch_bounds__(512, 2) void gemm_sk_kernel(GemmParams p, int total
         for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
           for (int mt = 0; mt < 8; ++mt)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[nt][mt]), rs, off0,
-                                                   (nt * 8 + mt) * 1024, 16);
+            buffer_store_b128<16>(__builtin_bit_cast(u32x4, acc[nt][mt]), rs, off0,
+                                  (nt * 8 + mt) * 1024);
         wait_vmcnt0();  // every storing wave drained
         big8_bar();
         if (tid == 0) __hip_atomic_store(flag, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -296,14 +296,14 @@ __device__ __forceinline__ void mx8_epilogue(const Mx8GemmParams& p, const f32x4
       } else if constexpr ((FL & EPI_OUT_F32) != 0) {
         if (ok) {
           float* c = (float*)p.C + (int64_t)m * p.ldc + n;
-          *(f32x4*)c = lo;
-          *(f32x4*)(c + 4) = hi;
+          store_f32x4(c, lo);
+          store_f32x4(c + 4, hi);
         }
       } else {
         if (ok) {
           const bf16x8 o = {(bf16)lo[0], (bf16)lo[1], (bf16)lo[2], (bf16)lo[3],
                             (bf16)hi[0], (bf16)hi[1], (bf16)hi[2], (bf16)hi[3]};
-          *(bf16x8*)((bf16*)p.C + (int64_t)m * p.ldc + n) = o;
+          store_bf16x8((bf16*)p.C + (int64_t)m * p.ldc + n, o);
         }
       }
     }

@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) void patchify_kernel(const float* __restrict__
   const int per_c = ps * HW;  // multiple of 4 (HW % 4 == 0 checked on host)
   for (int c = 0; c < C; ++c) {
     const float* src = img + (((int64_t)b * C + c) * HW + (int64_t)hh * ps) * HW;
-    for (int i = tid * 4; i < per_c; i += 256 * 4) *(f32x4*)(strip + c * per_c + i) = load4(src + i);
+    for (int i = tid * 4; i < per_c; i += 256 * 4) *(f32x4*)(strip + c * per_c + i) = load4(src + i);  // LDS
   }
   __syncthreads();
   const int pd = ps * ps * C;  // patch vector length
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(256) void patchify_cm_kernel(const float* __restric
   const int per_c = ps * HW;
   for (int c = 0; c < C; ++c) {
     const float* src = img + (((int64_t)b * C + c) * HW + (int64_t)hh * ps) * HW;
-    for (int i = tid * 4; i < per_c; i += 256 * 4) *(f32x4*)(strip + c * per_c + i) = load4(src + i);
+    for (int i = tid * 4; i < per_c; i += 256 * 4) *(f32x4*)(strip + c * per_c + i) = load4(src + i);  // LDS
   }
   __syncthreads();
   const int pd = ps * ps * C;
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void patchify_cm_kernel(const float* __restric
     if constexpr (std::is_same<TO, bf16>::value) {  // one 16-B store per 8 pixels
       const bf16x8 o = {(bf16)v0[0], (bf16)v0[1], (bf16)v0[2], (bf16)v0[3],
                         (bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
-      *(bf16x8*)op = o;
+      store_bf16x8(op, o);
     } else {
       store4(op, v0);
       store4(op + 4, v1);

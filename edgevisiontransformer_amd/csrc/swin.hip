@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256) void swin_patch_kernel(const float* __restrict
   const int np = S / ps, per_c = ps * S, pd = C * ps * ps;
   for (int c = 0; c < C; ++c) {
     const float* src = img + (((int64_t)b * C + c) * S + (int64_t)py * ps) * S;
-    for (int i = tid * 4; i < per_c; i += 256 * 4) *(f32x4*)(strip + c * per_c + i) = load4(src + i);
+    for (int i = tid * 4; i < per_c; i += 256 * 4) *(f32x4*)(strip + c * per_c + i) = load4(src + i);  // LDS
   }
   __syncthreads();
   TO* orow = out + ((int64_t)b * np + py) * np * ldo;
@@ -138,7 +138,7 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(const T* __restrict__ x, i
       s1 += f;
       s2 += f * f;
     }
-    if (live) *(u32x4*)(yr + c0) = *(const u32x4*)o;
+    if (live) store_b128(yr + c0, *(const u32x4*)o);
   }
 #pragma unroll
   for (int o = 1; o < LPR; o <<= 1) {
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256) void merge_kernel(const T* __restrict__ x, int
     const int q = e / cq, c = (e - q * cq) * V;
     const int y = 2 * oy + (q & 1), xx = 2 * ox + (q >> 1);
     const u32x4 v = *(const u32x4*)(x + ((int64_t)b * R * R + (int64_t)y * R + xx) * ldx + c);
-    *(u32x4*)(op + q * C + c) = v;
+    store_b128(op + q * C + c, v);
     const T* tv = (const T*)&v;
 #pragma unroll
     for (int j = 0; j < V; ++j) {

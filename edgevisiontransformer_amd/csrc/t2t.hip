@@ -488,7 +488,7 @@ __global__ __launch_bounds__(256) void unfold_k7s4c3_kernel(const float* __restr
       if constexpr (sizeof(TO) == 2) {
         const bf16x8 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3],
                           (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
-        *(u32x4*)op = __builtin_bit_cast(u32x4, o);
+        store_b128(op, __builtin_bit_cast(u32x4, o));
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const float q = (float)o[u];

@@ -1,0 +1,141 @@
+"""Repeated launches of every per-role kernel of the DeiT-base forward at a model shape that takes
+the same kernels as the benchmark (persistent 256x256 GEMM: >= 256 tiles; bs = 128, 25216 token
+rows): QKV (LN1 folded), out-proj (+ LN1(x) residual, statistics), FC1 (LN2 folded, GELU), FC2
+(+ LN2(xm) residual, statistics), the patch-embedding GEMM (bias + pos, CLS rows skipped) and the
+attention kernel. Reference ops: `attention.py:17-35`, `ffn.py:8-9`, `vit.py:45-51`.
+
+Each role: the first launch against a plain PyTorch fp32 reference of the same op (bf16 output
+tolerance), then REPEATS more launches that must equal the first bit for bit (the kernels are
+deterministic: no atomics, fixed reduction order). A wrong-result race like the round-2
+wide-store hazard (zeros in ~1 launch in 12) shows as a launch that differs; 16 repeats catch a
+1-in-12 rate with ~75 % probability per role, 6 roles together with > 99.9 %.
+"""
+import math
+
+import pytest
+import torch
+
+from edgevisiontransformer_amd import _lib
+from tests import _ops
+from tests.test_gpu_streamk import _gelu, _ln, _randn, _stats
+
+pytestmark = pytest.mark.gpu
+B, T, P, D, H, F = 128, 197, 196, 768, 12, 3072
+M = B * T
+REPEATS = 16
+
+
+def _repeat(launch, outs):
+    """launch() fills the tensors in `outs` (pre-poisoned by the caller); returns the first
+    launch's copies after checking every later launch against them bitwise"""
+    launch()
+    torch.cuda.synchronize()
+    first = [o.clone() for o in outs]
+    bad = []
+    for r in range(REPEATS):
+        for o in outs:
+            o.fill_(float("nan")) if o.dtype.is_floating_point else o.zero_()
+        launch()
+        torch.cuda.synchronize()
+        for i, (o, f) in enumerate(zip(outs, first)):
+            if not torch.equal(o, f):
+                n = int((o != f).sum())
+                bad.append((r, i, n))
+    assert not bad, f"launches differing from the first (launch, output, elements): {bad[:8]}"
+    return first
+
+
+def _lnin_case(N, gelu, seed):
+    x = (_randn((M, D), seed, 1.3) + 0.3).bfloat16()
+    g, be = 1.0 + _randn((D,), seed + 1, 0.1), _randn((D,), seed + 2, 0.1)
+    W, bias = _randn((D, N), seed + 3, 1 / math.sqrt(D)), _randn((N,), seed + 4, 0.05)
+    wp, kpad, npad = _ops.pack(W, "bf16", row_scale=g)
+    colsum, cvec = _ops.ln_fold("bf16", wp, kpad, npad, W, be, bias)
+    flags = _lib.EPI_LNIN | _lib.EPI_BIAS | (_lib.EPI_GELU if gelu else 0)
+    st = _stats(x)
+    C = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+
+    def launch():
+        _ops.dense("bf16", flags, x, wp, kpad, npad, M, N, bias=cvec, colsum=colsum,
+                   stats_in=st, ln_width=D, C=C)
+    (got,) = _repeat(launch, [C])
+    ref = _ln(x.float(), g, be) @ W + bias
+    if gelu:
+        ref = _gelu(ref)
+    torch.testing.assert_close(got.float(), ref, rtol=2.5e-2, atol=2.5e-2)
+
+
+def _resln_case(K, seed):
+    A = _randn((M, K), seed).bfloat16()
+    W, b = _randn((K, D), seed + 1, 1 / math.sqrt(K)), _randn((D,), seed + 2, 0.1)
+    x = (_randn((M, D), seed + 3, 1.1) - 0.2).bfloat16()
+    g, be = 1.0 + _randn((D,), seed + 4, 0.1), _randn((D,), seed + 5, 0.1)
+    wp, kpad, npad = _ops.pack(W, "bf16")
+    bias = torch.zeros(npad, device=A.device)
+    bias[:D] = b
+    rst = _stats(x)
+    so = torch.empty((M, 2 * ((D + 255) // 256), 2), device=A.device)
+    C = torch.empty((M, D), dtype=torch.bfloat16, device=A.device)
+    flags = _lib.EPI_BIAS | _lib.EPI_RESID | _lib.EPI_RESLN | _lib.EPI_STATS
+
+    def launch():
+        _ops.dense("bf16", flags, A, wp, kpad, npad, M, D, bias=bias, resid=x, rstats=rst,
+                   rgamma=g, rbeta=be, stats_out=so, ln_width=D, C=C)
+    got, st = _repeat(launch, [C, so])
+    ref = A.float() @ W.bfloat16().float() + b + _ln(x.float(), g, be)
+    torch.testing.assert_close(got.float(), ref, rtol=2e-2, atol=2e-2)
+    gf = got.float()
+    torch.testing.assert_close(st.sum(1)[:, 0], gf.sum(-1), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(st.sum(1)[:, 1], (gf * gf).sum(-1), rtol=1e-4, atol=1e-2)
+
+
+def test_repeat_qkv(gpu):
+    _lnin_case(3 * D, False, 100)
+
+
+def test_repeat_fc1(gpu):
+    _lnin_case(F, True, 110)
+
+
+def test_repeat_out_proj(gpu):
+    _resln_case(D, 120)
+
+
+def test_repeat_fc2(gpu):
+    _resln_case(F, 130)
+
+
+def test_repeat_patch_embed(gpu):
+    A = _randn((B * P, D), 140).bfloat16()
+    W, b = _randn((D, D), 141, 1 / 28.0), _randn((D,), 142, 0.1)
+    pos = _randn((P + 1, D), 143, 0.05)
+    wp, kpad, npad = _ops.pack(W, "bf16")
+    bias = torch.zeros(npad, device=A.device)
+    bias[:D] = b
+    pos_h = pos.bfloat16()
+    C = torch.empty((M, D), dtype=torch.bfloat16, device=A.device)
+    st = torch.empty((M, 2 * ((D + 255) // 256), 2), device=A.device)
+
+    def launch():
+        C[::T].fill_(7.0)   # CLS rows: never written by the patch GEMM
+        st[::T].fill_(-1.0)
+        _ops.dense("bf16", _lib.EPI_BIAS | _lib.EPI_POS | _lib.EPI_STATS, A, wp, kpad, npad,
+                   B * P, D, bias=bias, pos=pos, P=P, C=C, resid=pos_h, stats_out=st, ln_width=D)
+    got, _ = _repeat(launch, [C, st])
+    got = got.float().reshape(B, T, D)
+    assert torch.all(got[:, 0] == 7.0)
+    ref = (A.float() @ W.bfloat16().float() + b).reshape(B, P, D) + pos_h.float()[1:]
+    torch.testing.assert_close(got[:, 1:], ref, rtol=2e-2, atol=2e-2)
+
+
+def test_repeat_attention(gpu):
+    qkv = _randn((M, 3 * D), 150, 1.0).bfloat16()
+    out = torch.empty((M, D), dtype=torch.bfloat16, device=qkv.device)
+
+    def launch():
+        _ops.attention("bf16", qkv, B, T, H, out=out)
+    (got,) = _repeat(launch, [out])
+    q, k, v = qkv.float().reshape(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    p = torch.softmax(torch.einsum("bhid,bhjd->bhij", q, k) * 0.125, dim=-1)
+    ref = torch.einsum("bhij,bhjd->bhid", p, v).permute(0, 2, 1, 3).reshape(M, D)
+    torch.testing.assert_close(got.float(), ref, rtol=2e-2, atol=2e-2)
