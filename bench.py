@@ -9,19 +9,28 @@ attention, out-proj GEMM + residual, LN, FC1 GEMM + GELU, FC2 GEMM + residual] -
 libevt_hip.so, plus, for N > 1, the RCCL all-gather of every rank's logits (the only exchange step
 of the path: images are independent). Inputs are synthetic N(0,1) images already
 resident in HBM; weights are the deterministic random init (no checkpoints exist offline).
-Scaling is weak: each rank runs its own bs=512 batch.
+
+Scaling modes (N > 1):
+  weak (default)       each rank runs its own --batch images (512) per step: value = N*512/step;
+  strong               --global-batch G: one global batch of G images, sharded over the ranks by
+                       shard.sharded_forward (ceil/floor(G/N) per GPU), logits gathered by
+                       shard.gather_logits; value = G/step (global 512 -> 64/GPU).
+The process group has a timeout (--dist-timeout): a dead or hung peer ends the run with an error
+instead of a hang (failure detection).
 
 Extra objects on the JSON line:
-  roofline      the dominant kernel (FC1 GEMM, M = 512*197, K = 768, N = 3072, 31.8% of the
-                model's FLOPs; ties with FC2) timed INSIDE 5 real forwards after the timed region:
+  roofline      the dominant kernel (the role with the most device time; FC1 GEMM for DeiT-base,
+                M = 512*197, K = 768, N = 3072) timed INSIDE 5 real forwards after the timed region:
                 HIP events around each of its launches on the model's stream (evt_model_profile,
                 edgevisiontransformer_amd/profiling.py), so the figure agrees with a rocprofv3
-                kernel trace of the same command; achieved = 2*M*N*K / avg launch time vs the
-                2.5 PF dense bf16 MFMA peak. Also reported: per-role times of the forward
-                (--isolated-probe adds the same kernel launched alone back to back: it runs
-                hotter and ~20 % slower than inside the model).
+                kernel trace of the same command; achieved = its algorithmic FLOPs (or bytes, for
+                an HBM-bound role) / avg launch time vs the 2.5 PF dense bf16 MFMA peak (8 TB/s
+                HBM); hbm_frac = algorithmic bytes / time / 8 TB/s for every role (per_role);
+                traffic = HBM bytes per launch from the rocprofv3 PMC pass committed in
+                profiles/pmc_fc1.json (its build commit is reported beside it).
   cpu_baseline  the numpy fp32 restatement of the reference forward (oracle/, "port": TF is not
-                installed anywhere), DeiT-base bs=1 forwards for ~15 s on the host BLAS threads.
+                installed anywhere), bs=1 forwards of the same model for ~15 s on the host BLAS
+                threads.
 """
 from __future__ import annotations
 
@@ -40,6 +49,12 @@ sys.path.insert(0, REPO)
 
 PEAK_BF16_TFLOPS = 2516.6   # MI355X dense bf16 MFMA (spec; MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3     # MI355X fp32 matrix (spec)
+PEAK_HBM_GBPS = 8000.0      # MI355X HBM3E (spec; MI355X_MICROARCH.md)
+PMC_FILE = os.path.join(REPO, "profiles", "pmc_fc1.json")
+KERNEL_NAMES = {"fc1": "gemm_pers_kernel<LNIN|BIAS|GELU> (FC1)", "fc2": "gemm_pers_kernel<BIAS|RESID|RESLN|STATS> (FC2)",
+                "qkv": "gemm_pers_kernel<LNIN|BIAS> (QKV)", "attention": "attn_bf16_kernel",
+                "mlp": "swin_mlp96_kernel (stage-1 fused MLP)",
+                "attn_sublayer": "swin_attn96_kernel (stage-1 fused attention sublayer)"}
 METRIC = "images/sec DeiT-base/16-224 bs=512 @1/2/4/8 GPU; % bf16 MFMA roofline"
 
 
@@ -62,6 +77,10 @@ def parse():
                     help="evt_set_fusion flags (0 = separate kernels, 1 = fused QKV + attention)")
     ap.add_argument("--probe-only", type=int, default=0, metavar="N",
                     help="only launch the FC1 probe kernel N times and exit (PMC collection)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong scaling: shard ONE global batch of this many images over the ranks")
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="process-group (RCCL) timeout in seconds")
     return ap.parse_args()
 
 
@@ -153,20 +172,19 @@ def cpu_baseline(model_name: str, budget_s: float) -> dict:
 
 
 def pmc_traffic(M: int, K: int, N: int):
-    """HBM bytes per launch of the probe kernel from the committed rocprofv3 PMC summary
-    (scripts/gpu_pmc_fc1.sh -> profiles/*_pmc_fc1.json): 2 x FETCH_SIZE (gfx950 tallies 128-B
-    requests at 64 B, MI355X_MICROARCH.md HBM section) + WRITE_SIZE. None if absent or shape differs."""
-    import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_fc1.json")))
-    if not files:
-        return None
+    """HBM bytes per launch of the FC1 kernel from the rocprofv3 PMC pass committed as
+    profiles/pmc_fc1.json (scripts/gpu_pmc_fc1.sh: 2 x FETCH_SIZE, gfx950 tallies 128-B requests
+    at 64 B, MI355X_MICROARCH.md HBM section, + WRITE_SIZE) and the build commit it measured.
+    None if absent or collected at another shape."""
     try:
-        d = json.load(open(files[-1]))
+        d = json.load(open(PMC_FILE))
     except Exception:
-        return None
+        return None, None
     if (d.get("M"), d.get("K"), d.get("N")) != (M, K, N):
-        return None
-    return d.get("traffic_bytes_per_launch")
+        return None, None
+    return d.get("traffic_bytes_per_launch"), {"file": os.path.relpath(PMC_FILE, REPO),
+                                               "commit": d.get("commit"),
+                                               "collected": d.get("collected")}
 
 
 def main():
@@ -177,8 +195,10 @@ def main():
     torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
+        import datetime
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank),
+                                timeout=datetime.timedelta(seconds=args.dist_timeout))
 
     if args.probe_only:
         from edgevisiontransformer_amd.modeling.models.vit import _cfg_for
@@ -187,6 +207,7 @@ def main():
         print(json.dumps({"probe_us": round(t * 1e6, 1), "M": args.batch * cfg.tokens, "K": cfg.dim,
                           "N": cfg.ffn[0]}), flush=True)
         return
+    from edgevisiontransformer_amd import shard
     t2t = args.model.startswith("t2t")
     swin = args.model.startswith("swin")
     if swin:
@@ -195,24 +216,41 @@ def main():
         from edgevisiontransformer_amd.modeling.models import t2t_vit as mod
     else:
         from edgevisiontransformer_amd.modeling.models import vit as mod
-    model = mod.build_named(args.model, dtype=args.dtype, seed=0, max_batch=args.batch)
+    strong = args.global_batch > 0
+    if strong:  # this rank's shard of one global batch (shard.shard_range)
+        s0, s1 = shard.shard_range(args.global_batch, world, rank)
+        B, G = s1 - s0, args.global_batch
+        cap = -(-G // world)
+    else:
+        B, G, cap = args.batch, world * args.batch, args.batch
+    model = mod.build_named(args.model, dtype=args.dtype, seed=0, max_batch=cap)
     if args.fusion:
         from edgevisiontransformer_amd import _lib
         _lib.check(_lib.load_library().evt_set_fusion(args.fusion))
     if args.gemm_variant:
         from edgevisiontransformer_amd import _lib
         _lib.check(_lib.load_library().evt_set_gemm_variant(args.gemm_variant))
-    B = args.batch
-    g = torch.Generator(device="cuda").manual_seed(1000 + rank)
-    shape = (B, 224, 224, 3) if t2t else (B, 3, 224, 224)   # T2T-ViT is channel-last
-    img = torch.randn(shape, generator=g, device="cuda", dtype=torch.float32)
-    logits = torch.empty((B, model.num_classes), device="cuda", dtype=torch.float32)
-    gathered = torch.empty((world * B, model.num_classes), device="cuda") if world > 1 else None
+    shape = (224, 224, 3) if t2t else (3, 224, 224)   # T2T-ViT is channel-last
+    if strong:  # every rank holds the global batch (same seed): sharded_forward slices its shard
+        g = torch.Generator(device="cuda").manual_seed(1000)
+        gimg = torch.randn((G, *shape), generator=g, device="cuda", dtype=torch.float32)
+        img = gimg[s0:s1]
+    else:
+        g = torch.Generator(device="cuda").manual_seed(1000 + rank)
+        img = torch.randn((B, *shape), generator=g, device="cuda", dtype=torch.float32)
+    logits = torch.empty((max(B, 1), model.num_classes), device="cuda", dtype=torch.float32)
+    gathered = torch.empty((world * B, model.num_classes), device="cuda") if world > 1 and not strong else None
+
+    def local_forward(x):
+        return model.forward_into(x, logits[: x.shape[0]])
 
     def step():
-        model.forward_into(img, logits)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, logits)
+        if strong:
+            shard.sharded_forward(local_forward, gimg, world, rank)
+        else:
+            model.forward_into(img, logits)
+            if world > 1:
+                dist.all_gather_into_tensor(gathered, logits)
 
     for _ in range(args.warmup):
         step()
@@ -231,46 +269,63 @@ def main():
         t = torch.tensor([el], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    ok = bool(torch.isfinite(logits).all().item())
+    ok = bool(torch.isfinite(logits[:B]).all().item())
 
     gflop_img = model.cfg.gflop_per_image()
-    imgs_per_s = world * B * args.steps / el
+    imgs_per_s = G * args.steps / el
     peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
     roof = None
-    if rank == 0 and not args.no_probe and not swin:
-        # the dominant kernel (FC1) timed INSIDE real forwards: HIP events around each of its
-        # launches on the model's stream (evt_model_profile), after the timed region
-        from edgevisiontransformer_amd.profiling import kernel_times
-        kt = kernel_times(model, img, logits, forwards=5)
-        ffn = model.cfg.mlp_dim if t2t else model.cfg.ffn[0]
-        M, K, N = B * model.cfg.tokens, model.cfg.dim, ffn
-        t_k = kt["fc1"]["us_per_launch"] * 1e-6
-        ach = 2.0 * M * N * K / t_k / 1e12
-        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(ach / peak, 4), "traffic": pmc_traffic(M, K, N),
-                "kernel": f"gemm_pers_kernel<LNIN|BIAS|GELU> (FC1, {args.dtype}) M={M} K={K} N={N}",
-                "avg_launch_us": round(t_k * 1e6, 1), "launches_timed": 5 * kt["fc1"]["launches"],
-                "timing": "HIP events around each FC1 launch inside 5 forwards (evt_model_profile)",
-                "per_role_us": {k: round(v["us_per_launch"], 1) for k, v in kt.items()}}
-        if args.isolated_probe:  # off by default: its launches would mix into a rocprof average
-            roof["isolated_probe_us"] = round(kernel_probe(args.dtype, M, K, N) * 1e6, 1)
+    if rank == 0 and not args.no_probe:
+        # every role's kernels timed INSIDE real forwards (HIP events around each launch on the
+        # model's stream, evt_model_profile) with their algorithmic work, after the timed region
+        from edgevisiontransformer_amd.profiling import kernel_times, roofline_table
+        kt = kernel_times(model, img, logits[:B], forwards=5)
+        table = roofline_table(kt, peak, PEAK_HBM_GBPS)
+        dom = max(kt, key=lambda r: kt[r]["us_per_forward"])
+        k = kt[dom]
+        t_k = k["us_per_launch"] * 1e-6
+        fl, by = k["gflop"] * 1e9 / k["launches"], k["gbytes"] * 1e9 / k["launches"]
+        mfma_bound = fl / peak / 1e12 >= by / PEAK_HBM_GBPS / 1e9
+        ach = fl / t_k / 1e12 if mfma_bound else by / t_k / 1e9
+        roof = {"bound": "mfma" if mfma_bound else "hbm", "achieved": round(ach, 2),
+                "peak": peak if mfma_bound else PEAK_HBM_GBPS,
+                "unit": "TFLOP/s" if mfma_bound else "GB/s",
+                "frac": round(ach / (peak if mfma_bound else PEAK_HBM_GBPS), 4),
+                "traffic": None, "role": dom,
+                "kernel": f"{KERNEL_NAMES.get(dom, dom)} ({args.model}, {args.dtype})",
+                "algorithmic_flop_per_launch": fl, "algorithmic_bytes_per_launch": by,
+                "hbm_gbps": round(by / t_k / 1e9, 1),
+                "hbm_frac": round(by / t_k / 1e9 / PEAK_HBM_GBPS, 4),
+                "mfma_frac": round(fl / t_k / 1e12 / peak, 4),
+                "avg_launch_us": round(t_k * 1e6, 1), "launches_timed": 5 * k["launches"],
+                "timing": "HIP events around each launch of the role inside 5 forwards "
+                          "(evt_model_profile)",
+                "per_role": table}
+        if dom == "fc1" and not t2t and not swin:
+            M, K, N = B * model.cfg.tokens, model.cfg.dim, model.cfg.ffn[0]
+            roof["kernel"] += f" M={M} K={K} N={N}"
+            roof["traffic"], roof["traffic_source"] = pmc_traffic(M, K, N)
+            if args.isolated_probe:  # off by default: its launches would mix into a rocprof average
+                roof["isolated_probe_us"] = round(kernel_probe(args.dtype, M, K, N) * 1e6, 1)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(args.model, args.cpu_seconds)
     if rank == 0:
+        par = "dp1" if world == 1 else (
+            f"dp{world} (one global batch of {G} sharded {B}-{cap} per GPU, RCCL all-gather of logits)"
+            if strong else f"dp{world} (batch shard, RCCL all-gather of logits)")
         out = {
             "metric": METRIC if args.model == "deit_base" else f"images/sec {args.model} bs={B}",
             "value": round(imgs_per_s, 2), "unit": "images/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
-            "data": "synthetic N(0,1) NCHW images resident in HBM; deterministic random-init weights",
-            "config": {"workload": f"{args.model}/{'224' if t2t or swin else '16-224'} forward, bs={B} per "
-                                   f"GPU, {args.dtype}",
-                       "model": args.model, "global_batch": world * B, "per_gpu_batch": B,
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic N(0,1) images resident in HBM; deterministic random-init weights",
+            "config": {"workload": f"{args.model}/{'224' if t2t or swin else '16-224'} forward, "
+                                   f"bs={cap} per GPU, {args.dtype}",
+                       "model": args.model, "global_batch": G, "per_gpu_batch": cap,
                        "seq_len": model.cfg.res(0) ** 2 if swin else model.cfg.tokens,
-                       "parallelism": f"dp{world} (batch shard, "
-                       "RCCL all-gather of logits)" if world > 1 else "dp1"},
+                       "parallelism": par},
             "model_roofline": {"achieved_tflops": round(imgs_per_s * gflop_img / world / 1e3, 2),
                                "peak": peak, "frac": round(imgs_per_s * gflop_img / world / 1e3
                                                            / peak, 4),

@@ -30,7 +30,8 @@ EPI_OUT_MX8 = 512
 FUSE_QKV_ATTENTION = 1  # evt_set_fusion flag (include/evt.h EVT_FUSE_QKV_ATTENTION)
 # evt_model_profile roles (include/evt.h EVT_PROF_*)
 PROF_ROLES = ("patchify", "patch_embed", "qkv", "attention", "out_proj", "fc1", "fc2", "head",
-              "qkv_attention")
+              "qkv_attention", "t2t_unfold", "t2t_kqv", "t2t_performer", "merge", "attn_sublayer",
+              "mlp")
 SWIN_MAX_STAGES = 8
 
 
@@ -114,6 +115,7 @@ SIGNATURES = {
     "evt_set_fusion": (_I, [_I]),
     "evt_model_profile": (_I, [_P, _I]),
     "evt_model_profile_read": (_I, [_P, _P, _P]),
+    "evt_model_profile_work": (_I, [_P, _P, _P]),
     "evt_qkv_attention": (_I, [_P, _I, _P, _P, _P, _P, _I, _I, _I, _F, _F, _P, _I64, _P]),
     "evt_pack_weight": (_I, [_I, _P, _P, _I, _I, _P, _I, _I, _P]),
     "evt_ln_fold": (_I, [_I, _P, _I, _I, _P, _P, _P, _I, _I, _P, _P, _P]),

@@ -156,6 +156,8 @@ struct evt_model {
   bool prof = false;
   std::vector<hipEvent_t> prof_ev;   // pool (pairs)
   std::vector<int> prof_role;        // role of pair i of the last forward
+  // algorithmic work of pair i (evt_model_profile_work): GFLOP and GB its kernels must do / move
+  mutable std::vector<double> prof_gflop, prof_gbytes;
 };
 
 namespace {
@@ -180,6 +182,8 @@ struct ProfScope {
       m->prof_ev.push_back(e);
     }
     m->prof_role.push_back(role);
+    m->prof_gflop.push_back(0.0);
+    m->prof_gbytes.push_back(0.0);
     (void)hipEventRecord(m->prof_ev[2 * pair], s);
   }
   ~ProfScope() {
@@ -187,7 +191,16 @@ struct ProfScope {
   }
 };
 void prof_reset(evt_model* m) {
-  if (m->prof) m->prof_role.clear();
+  if (!m->prof) return;
+  m->prof_role.clear();
+  m->prof_gflop.clear();
+  m->prof_gbytes.clear();
+}
+// add algorithmic work (flops, bytes) to the innermost open ProfScope of a profiled forward
+void prof_work(const evt_model* m, double flops, double bytes) {
+  if (!m->prof || m->prof_gflop.empty()) return;
+  m->prof_gflop.back() += flops * 1e-9;
+  m->prof_gbytes.back() += bytes * 1e-9;
 }
 
 int dev_alloc(evt_model* m, void** p, size_t bytes) {
@@ -347,7 +360,26 @@ struct DenseCall {
   int slot_width = 0;  // width whose stats_slots() numbers the slots (0: ln_width)
 };
 
+// Algorithmic work of one Dense launch: 2 M K N with the layer's real K and N; bytes = A and W
+// read once, C written once, plus the residual, the row statistics read / written and the small
+// bias / position vectors (what the kernel cannot avoid moving).
+void dense_work(const evt_model* m, const DenseW& w, const DenseCall& c) {
+  if (!m->prof) return;
+  const double es = (double)elem_size(m->dtype);
+  const double M = c.M, K = w.K, N = std::min(c.N, w.N);
+  const int width = c.ln_width ? c.ln_width : m->D;
+  const double slot_row = (double)stats_slots(c.slot_width ? c.slot_width : width) * 8.0;
+  double bytes = M * K * es + K * N * es + M * N * ((c.flags & EPI_OUT_F32) ? 4.0 : es) + 8.0 * N;
+  if (c.flags & EPI_RESID) bytes += M * N * es;
+  if (c.flags & EPI_LNIN) bytes += M * slot_row;
+  if (c.flags & EPI_RESLN) bytes += M * slot_row + 8.0 * N;
+  if (c.flags & EPI_STATS) bytes += M * slot_row;
+  if (c.flags & EPI_POS) bytes += (double)(c.P + 1) * N * 4.0;
+  prof_work(m, 2.0 * M * K * N, bytes);
+}
+
 int dense(const evt_model* m, const DenseW& w, const DenseCall& c, hipStream_t s) {
+  dense_work(m, w, c);
   GemmParams p{};
   p.A = c.A;
   p.lda = c.lda;
@@ -456,6 +488,7 @@ int dense_head(const evt_model* m, const DenseW& w, const DenseCall& c, hipStrea
   if (S < 2 || !m->hbuf || part > m->hbuf_bytes ||
       (c.flags & ~(EPI_BIAS | EPI_GELU | EPI_OUT_F32)))
     return dense(m, w, c, s);
+  dense_work(m, w, c);
   GemmParams p{};
   p.A = c.A; p.lda = c.lda; p.W = w.w; p.ldw = w.kpad; p.C = c.C; p.ldc = c.ldc;
   p.M = c.M; p.N = c.N; p.K = w.kpad; p.ntiles = w.npad / GEMM_BN; p.bias = w.b;
@@ -472,6 +505,9 @@ int run_encoder(evt_model* m, int B, hipStream_t s) {
   for (const Layer& L : m->layers) {
     if (fuse) {  // LN1-folded QKV + attention in one kernel (qkv_attn.hip)
       ProfScope ps(m, EVT_PROF_QKV_ATTENTION, s);
+      prof_work(m, 2.0 * rows * D * 3 * L.inner + 4.0 * B * L.heads * (double)T * T * 64,
+                (double)rows * (D + L.inner) * elem_size(m->dtype) +
+                    (double)D * 3 * L.inner * elem_size(m->dtype) + rows * stats_slots(D) * 8.0);
       QkvAttnParams p{};
       p.x = m->x; p.ldx = D; p.stats = m->sx; p.nslots = stats_slots(D);
       p.inv_d = 1.0f / (float)D; p.eps = m->eps;
@@ -489,6 +525,8 @@ int run_encoder(evt_model* m, int B, hipStream_t s) {
         EVT_RC(dense(m, L.qkv, c, s));
       }
       ProfScope ps(m, EVT_PROF_ATTENTION, s);
+      prof_work(m, 4.0 * B * L.heads * (double)T * T * 64,
+                (double)rows * 4 * L.inner * elem_size(m->dtype));  // qkv read + O written
       AttnParams ap{m->qkv, 3 * L.inner, m->o, L.inner, T, L.heads, B, 0.125f * log2e};
       EVT_HIP(attention_launch(m->dtype, ap, s), "attention");
     }
@@ -850,6 +888,9 @@ int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* 
   // patch embedding (vit.py:45-51): rearrange -> Dense(D) + pos, CLS row = cls + pos[0]
   {
     ProfScope ps(m, EVT_PROF_PATCHIFY, s);
+    prof_work(m, 0.0, (double)B * d.in_chans * d.image_size * d.image_size * 4 +
+                          (double)B * (sh.P * sh.pd + D) * elem_size(dt) +
+                          (double)B * stats_slots(D) * 8);  // image read, patch rows + CLS rows
     EVT_HIP(patchify_launch(dt, img, B, d.in_chans, d.image_size, d.patch_size, m->apatch, m->x,
                             m->cls, m->pos, D, m->sx, s, m->patch_cm),
             "patchify");
@@ -981,38 +1022,68 @@ int evt_t2t_forward(evt_model* m, const float* img, int B, float* logits, void* 
   const int g1 = m->grid[0], g2 = m->grid[1];
   const int t1 = g1 * g1, t2 = g2 * g2;
   // iteration 1: soft_split0 (k7 s4 p2) of the NHWC image -> TokenPerformer    (t2t_vit.py:66-68)
+  const double es = (double)elem_size(dt);
+  // performer core per token (transformer_encoder.py:67-99): prm_exp of k and q (2 x 64x32),
+  // D (32), kptv (32x64), y (32x64), attn_output Dense (64x64), FFN (2 x 64x64)
+  const double perf_flops = 2.0 * (2 * 64 * 32 + 32 + 32 * 64 + 32 * 64 + 3 * 64 * 64);
   const Performer& P1 = m->perf[0];
-  EVT_HIP(unfold_launch(dt, 1, img, B, S, S, d.in_chans, 7, 4, 2, m->u, P1.dpad, m->su,
-                        stats_slots(P1.din), s),
-          "soft_split0");
   {
+    ProfScope ps(m, EVT_PROF_T2T_UNFOLD, s);
+    prof_work(m, 0.0, (double)B * S * S * d.in_chans * 4 + (double)B * t1 * P1.din * es +
+                          (double)B * t1 * stats_slots(P1.din) * 8);
+    EVT_HIP(unfold_launch(dt, 1, img, B, S, S, d.in_chans, 7, 4, 2, m->u, P1.dpad, m->su,
+                          stats_slots(P1.din), s),
+            "soft_split0");
+  }
+  {
+    ProfScope ps(m, EVT_PROF_T2T_KQV, s);
     DenseCall c;
     c.flags = EPI_LNIN | EPI_BIAS;
     c.A = m->u; c.lda = P1.dpad; c.C = m->kqvb; c.ldc = 3 * 64; c.M = B * t1; c.N = 3 * 64;
     c.stats_in = m->su; c.ln_width = P1.din;
     EVT_RC(dense(m, P1.kqv, c, s));
   }
-  EVT_HIP(performer_launch(dt, m->kqvb, 3 * 64, B, t1, P1.w, m->part, m->pout, 64, s),
-          "performer1");
+  {
+    ProfScope ps(m, EVT_PROF_T2T_PERFORMER, s);
+    prof_work(m, perf_flops * B * t1, (double)B * t1 * (3 * 64 + 64) * es);
+    EVT_HIP(performer_launch(dt, m->kqvb, 3 * 64, B, t1, P1.w, m->part, m->pout, 64, s),
+            "performer1");
+  }
   // iteration 2: soft_split1 (k3 s2 p1) of the [B, S/4, S/4, 64] map -> TokenPerformer (:72-77)
   const Performer& P2 = m->perf[1];
-  EVT_HIP(unfold_launch(dt, 0, m->pout, B, g1, g1, 64, 3, 2, 1, m->u, P2.dpad, m->su,
-                        stats_slots(P2.din), s),
-          "soft_split1");
   {
+    ProfScope ps(m, EVT_PROF_T2T_UNFOLD, s);
+    prof_work(m, 0.0, (double)B * t1 * 64 * es + (double)B * t2 * P2.din * es +
+                          (double)B * t2 * stats_slots(P2.din) * 8);
+    EVT_HIP(unfold_launch(dt, 0, m->pout, B, g1, g1, 64, 3, 2, 1, m->u, P2.dpad, m->su,
+                          stats_slots(P2.din), s),
+            "soft_split1");
+  }
+  {
+    ProfScope ps(m, EVT_PROF_T2T_KQV, s);
     DenseCall c;
     c.flags = EPI_LNIN | EPI_BIAS;
     c.A = m->u; c.lda = P2.dpad; c.C = m->kqvb; c.ldc = 3 * 64; c.M = B * t2; c.N = 3 * 64;
     c.stats_in = m->su; c.ln_width = P2.din;
     EVT_RC(dense(m, P2.kqv, c, s));
   }
-  EVT_HIP(performer_launch(dt, m->kqvb, 3 * 64, B, t2, P2.w, m->part, m->pout, 64, s),
-          "performer2");
-  // soft_split2 -> project Dense(D) into token rows 1..P, + CLS row, + sinusoid pos (:81-86,121-125)
-  EVT_HIP(unfold_launch(dt, 0, m->pout, B, g2, g2, 64, 3, 2, 1, m->u, 9 * 64, nullptr, 0, s),
-          "soft_split2");
-  EVT_HIP(cls_rows_launch(dt, m->x, B, T, D, m->cls, m->pos, m->sx, s), "cls rows");
   {
+    ProfScope ps(m, EVT_PROF_T2T_PERFORMER, s);
+    prof_work(m, perf_flops * B * t2, (double)B * t2 * (3 * 64 + 64) * es);
+    EVT_HIP(performer_launch(dt, m->kqvb, 3 * 64, B, t2, P2.w, m->part, m->pout, 64, s),
+            "performer2");
+  }
+  // soft_split2 -> project Dense(D) into token rows 1..P, + CLS row, + sinusoid pos (:81-86,121-125)
+  {
+    ProfScope ps(m, EVT_PROF_T2T_UNFOLD, s);
+    prof_work(m, 0.0, (double)B * t2 * 64 * es + (double)B * P * 9 * 64 * es);
+    EVT_HIP(unfold_launch(dt, 0, m->pout, B, g2, g2, 64, 3, 2, 1, m->u, 9 * 64, nullptr, 0, s),
+            "soft_split2");
+  }
+  {
+    ProfScope ps(m, EVT_PROF_PATCH_EMBED, s);
+    prof_work(m, 0.0, (double)B * D * es + (double)B * stats_slots(D) * 8);
+    EVT_HIP(cls_rows_launch(dt, m->x, B, T, D, m->cls, m->pos, m->sx, s), "cls rows");
     DenseCall c;
     c.flags = EPI_BIAS | EPI_POS | EPI_STATS;
     c.A = m->u; c.lda = 9 * 64; c.C = m->x; c.ldc = D; c.M = B * P; c.N = D;
@@ -1021,6 +1092,7 @@ int evt_t2t_forward(evt_model* m, const float* img, int B, float* logits, void* 
   }
   EVT_RC(run_encoder(m, B, s));  // :127
   {  // LayerNorm of the CLS rows folded into the classifier (:129-134)
+    ProfScope ps(m, EVT_PROF_HEAD, s);
     DenseCall c;
     c.flags = EPI_LNIN | EPI_BIAS | EPI_OUT_F32;
     c.A = m->x; c.lda = (int64_t)T * D; c.C = logits; c.ldc = d.num_classes; c.M = B;
@@ -1035,6 +1107,8 @@ int evt_model_profile(evt_model* m, int enable) {
   if (m->graph && enable) return fail(EVT_EINVAL, "profiling a model with a captured graph");
   m->prof = enable != 0;
   m->prof_role.clear();
+  m->prof_gflop.clear();
+  m->prof_gbytes.clear();
   return EVT_OK;
 }
 
@@ -1054,8 +1128,20 @@ int evt_model_profile_read(evt_model* m, float* us, int* launches) {
   return EVT_OK;
 }
 
+int evt_model_profile_work(evt_model* m, double* gflop, double* gbytes) {
+  if (!m || !gflop || !gbytes) return fail(EVT_EINVAL, "null argument");
+  for (int r = 0; r < EVT_PROF_ROLES; ++r) gflop[r] = gbytes[r] = 0.0;
+  for (size_t i = 0; i < m->prof_role.size(); ++i) {
+    gflop[m->prof_role[i]] += m->prof_gflop[i];
+    gbytes[m->prof_role[i]] += m->prof_gbytes[i];
+  }
+  return EVT_OK;
+}
+
 int evt_graph_capture(evt_model* m, const float* img, int batch, float* logits, void* stream) {
   if (!m || !stream) return fail(EVT_EINVAL, "graph capture needs a model and a non-NULL stream");
+  if (m->prof)  // the events would be captured into the graph, never recorded on the stream
+    return fail(EVT_EINVAL, "graph capture while profiling is enabled (evt_model_profile(m, 0) first)");
   hipStream_t s = (hipStream_t)stream;
   if (m->graph_exec) {
     (void)hipGraphExecDestroy(m->graph_exec);
@@ -1207,23 +1293,33 @@ int evt_swin_forward(evt_model* m, const float* img, int B, float* logits, void*
   const float scale_log2 = 0.17677669529663687f * 1.4426950408889634f;  // 32^-0.5 * log2(e)
   // patch embed: Conv2d(k = s = patch) as im2col + Dense, then its LayerNorm -> stream x + stats
   int rows = B * s0.R * s0.R;
-  EVT_HIP(swin_patch_launch(dt, img, B, d.in_chans, d.image_size, d.patch_size, m->hbuf, pdst, s),
-          "patch im2col");
+  const double es = (double)elem_size(dt);
   {
+    ProfScope ps(m, EVT_PROF_PATCHIFY, s);
+    prof_work(m, 0.0, (double)B * d.in_chans * d.image_size * d.image_size * 4 +
+                          (double)rows * d.in_chans * d.patch_size * d.patch_size * es);
+    EVT_HIP(swin_patch_launch(dt, img, B, d.in_chans, d.image_size, d.patch_size, m->hbuf, pdst, s),
+            "patch im2col");
+  }
+  {
+    ProfScope ps(m, EVT_PROF_PATCH_EMBED, s);
     DenseCall c;
     c.flags = EPI_BIAS;
     c.A = m->hbuf; c.lda = pdst; c.C = m->xm; c.ldc = s0.Cst; c.M = rows; c.N = s0.Cst;
     EVT_RC(dense(m, m->patch, c, s));
+    prof_work(m, 0.0, 2.0 * rows * s0.C * es + (double)rows * stats_slots(s0.C) * 8);
+    EVT_HIP(ln_rows_launch(dt, m->xm, s0.Cst, m->x, m->pnorm_g, m->pnorm_b, rows, s0.C, 1e-5f,
+                           m->sx, stats_slots(s0.C), s),
+            "patch norm");
   }
-  EVT_HIP(ln_rows_launch(dt, m->xm, s0.Cst, m->x, m->pnorm_g, m->pnorm_b, rows, s0.C, 1e-5f, m->sx,
-                         stats_slots(s0.C), s),
-          "patch norm");
   for (size_t i = 0; i < m->stages.size(); ++i) {
     const SwinStage& st = m->stages[i];
     const int C = st.C, Cst = st.Cst;
     rows = B * st.R * st.R;
     if (i > 0) {  // PatchMerging: gather -> LN(4C)-folded reduction -> stream x (+ stats)
       const SwinStage& pv = m->stages[i - 1];
+      ProfScope ps(m, EVT_PROF_MERGE, s);
+      prof_work(m, 0.0, 2.0 * rows * 4 * pv.C * es + (double)rows * stats_slots(C) * 8);
       EVT_HIP(merge_launch(dt, m->x, pv.Cst, B, pv.R, pv.C, m->hbuf, m->sm, stats_slots(C), s),
               "patch merge");
       DenseCall c;
@@ -1234,21 +1330,33 @@ int evt_swin_forward(evt_model* m, const float* img, int B, float* logits, void*
     }
     for (const SwinBlock& bl : st.blocks) {
       const bool fuse96 = dt == DT_BF16 && C == 96 && st.H == 3 && gemm_variant() == 0;
+      const double slot_rows = (double)rows * stats_slots(C) * 8;
       if (fuse96) {  // stage-1 attention sublayer fused (swin.hip, swin_attn96_kernel)
+        ProfScope ps(m, EVT_PROF_ATTN_SUBLAYER, s);
+        prof_work(m, 2.0 * rows * C * 4 * C + 4.0 * rows * 49 * C,
+                  2.0 * rows * C * es + 2 * slot_rows + 4.0 * C * C * es);
         SwinAttnBlockParams ab{m->x, m->xm, m->sx, m->sm, bl.qkv.w, bl.qkv.b, bl.proj.w,
                                bl.proj.b, bl.bias, bl.qkv.kpad, bl.proj.kpad, B, st.R, bl.shift,
                                stats_slots(C), m->eps};
         EVT_HIP(swin_attn96_launch(ab, s), "fused window attention sublayer");
       }
       if (!fuse96) {  // LN1-folded QKV (+ bias)
-        DenseCall c;
-        c.flags = EPI_LNIN | EPI_BIAS;
-        c.A = m->x; c.lda = Cst; c.C = m->qkv; c.ldc = 3 * C; c.M = rows; c.N = 3 * C;
-        c.stats_in = m->sx; c.ln_width = C;
-        EVT_RC(dense(m, bl.qkv, c, s));
-        SwinAttnParams ap{m->qkv, 3 * C, m->o, Cst, bl.bias, B, st.R, st.R / 7, C, st.H, bl.shift,
-                          scale_log2};
-        EVT_HIP(window_attn_launch(dt, ap, s), "window attention");
+        {
+          ProfScope ps(m, EVT_PROF_QKV, s);
+          DenseCall c;
+          c.flags = EPI_LNIN | EPI_BIAS;
+          c.A = m->x; c.lda = Cst; c.C = m->qkv; c.ldc = 3 * C; c.M = rows; c.N = 3 * C;
+          c.stats_in = m->sx; c.ln_width = C;
+          EVT_RC(dense(m, bl.qkv, c, s));
+        }
+        {
+          ProfScope ps(m, EVT_PROF_ATTENTION, s);
+          prof_work(m, 4.0 * rows * 49 * C, 4.0 * rows * C * es);  // 49 keys per query
+          SwinAttnParams ap{m->qkv, 3 * C, m->o, Cst, bl.bias, B, st.R, st.R / 7, C, st.H,
+                            bl.shift, scale_log2};
+          EVT_HIP(window_attn_launch(dt, ap, s), "window attention");
+        }
+        ProfScope ps(m, EVT_PROF_OUT_PROJ, s);
         DenseCall pc;  // proj + bias + residual x -> xm (+ stats)
         pc.flags = EPI_BIAS | EPI_RESID | EPI_STATS;
         pc.A = m->o; pc.lda = Cst; pc.C = m->xm; pc.ldc = Cst; pc.M = rows; pc.N = Cst;
@@ -1257,6 +1365,9 @@ int evt_swin_forward(evt_model* m, const float* img, int B, float* logits, void*
       }
       if (dt == DT_BF16 && C == 96 && st.mlp == 384 && gemm_variant() == 0) {
         // stage-1 MLP (C = 96) fused: hidden kept on chip (swin.hip, swin_mlp96_kernel)
+        ProfScope ps(m, EVT_PROF_MLP, s);
+        prof_work(m, 4.0 * rows * C * st.mlp, 2.0 * rows * C * es + 2 * slot_rows +
+                                                   2.0 * C * st.mlp * es);
         SwinMlpParams mp{m->xm, m->x, m->sm, m->sx, bl.fc1.w, bl.fc1.colsum, bl.fc1.b,
                          bl.fc2.w, bl.fc2.b, bl.fc1.kpad, bl.fc2.kpad, rows, stats_slots(C),
                          m->eps};
@@ -1264,6 +1375,7 @@ int evt_swin_forward(evt_model* m, const float* img, int B, float* logits, void*
         continue;
       }
       {  // LN2-folded FC1 + erf GELU
+        ProfScope ps(m, EVT_PROF_FC1, s);
         DenseCall c;
         c.flags = EPI_LNIN | EPI_BIAS | EPI_GELU_ERF;
         c.A = m->xm; c.lda = Cst; c.C = m->hbuf; c.ldc = st.mst; c.M = rows; c.N = st.mst;
@@ -1271,6 +1383,7 @@ int evt_swin_forward(evt_model* m, const float* img, int B, float* logits, void*
         EVT_RC(dense(m, bl.fc1, c, s));
       }
       {  // FC2 + bias + residual xm -> x (+ stats)
+        ProfScope ps(m, EVT_PROF_FC2, s);
         DenseCall c;
         c.flags = EPI_BIAS | EPI_RESID | EPI_STATS;
         c.A = m->hbuf; c.lda = st.mst; c.C = m->x; c.ldc = Cst; c.M = rows; c.N = Cst;
@@ -1281,6 +1394,9 @@ int evt_swin_forward(evt_model* m, const float* img, int B, float* logits, void*
   }
   // final LayerNorm + mean over tokens -> head Dense (fp32 logits)
   const SwinStage& sl = m->stages.back();
+  ProfScope ps_head(m, EVT_PROF_HEAD, s);
+  prof_work(m, 0.0, (double)B * sl.R * sl.R * sl.C * es + (double)B * sl.R * sl.R * stats_slots(sl.C) * 8 +
+                        (double)B * sl.C * es);
   EVT_HIP(ln_pool_launch(dt, m->x, sl.Cst, B, sl.R * sl.R, sl.C, m->sx, stats_slots(sl.C),
                          m->norm_g, m->norm_b, m->pooled, sl.Cst, s),
           "norm + avgpool");

@@ -8,10 +8,15 @@ evaluation (`deit_pruning/src/utils.py:151-228`: DistributedSampler shards, then
 """
 from __future__ import annotations
 
+import datetime
 from typing import Callable, Optional, Tuple
 
 import torch
 import torch.distributed as dist
+
+
+class GatherTimeout(TimeoutError):
+    """A rank's logits gather did not complete within its timeout (a peer is dead or hung)."""
 
 
 def shard_range(global_batch: int, world: int, rank: int) -> Tuple[int, int]:
@@ -25,11 +30,15 @@ def shard_range(global_batch: int, world: int, rank: int) -> Tuple[int, int]:
 
 
 def gather_logits(local: torch.Tensor, global_batch: int, world: int,
-                  group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+                  group: Optional[dist.ProcessGroup] = None,
+                  timeout: Optional[float] = None) -> torch.Tensor:
     """All-gather every rank's [n_r, C] logits into [global_batch, C] in rank order.
 
     Shards may be uneven by one row; each rank pads to the largest shard so a single
     all_gather_into_tensor moves ceil(B/G)*C*4 bytes per rank.
+    timeout (seconds): wait for the collective at most this long, then raise GatherTimeout
+    instead of blocking forever on a dead peer (failure detection; the process
+    group's own timeout, set at init_process_group, bounds it as well).
     """
     if world == 1:
         return local
@@ -38,7 +47,18 @@ def gather_logits(local: torch.Tensor, global_batch: int, world: int,
     buf = torch.zeros((cap, C), dtype=local.dtype, device=local.device)
     buf[: local.shape[0]] = local
     out = torch.empty((world * cap, C), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(out, buf, group=group)
+    if timeout is None:
+        dist.all_gather_into_tensor(out, buf, group=group)
+    else:
+        work = dist.all_gather_into_tensor(out, buf, group=group, async_op=True)
+        try:
+            done = work.wait(timeout=datetime.timedelta(seconds=timeout))
+        except Exception as e:  # gloo raises on timeout; NCCL aborts the communicator
+            raise GatherTimeout(f"rank {dist.get_rank(group)}: logits gather did not complete "
+                                f"within {timeout:.1f} s ({type(e).__name__}: {e})") from e
+        if done is False:
+            raise GatherTimeout(f"rank {dist.get_rank(group)}: logits gather did not complete "
+                                f"within {timeout:.1f} s")
     rows = []
     for r in range(world):
         s, e = shard_range(global_batch, world, r)
@@ -47,8 +67,9 @@ def gather_logits(local: torch.Tensor, global_batch: int, world: int,
 
 
 def sharded_forward(forward: Callable[[torch.Tensor], torch.Tensor], images: torch.Tensor,
-                    world: int, rank: int, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+                    world: int, rank: int, group: Optional[dist.ProcessGroup] = None,
+                    timeout: Optional[float] = None) -> torch.Tensor:
     """Run `forward` on this rank's shard of `images` (global batch) and gather all logits."""
     s, e = shard_range(images.shape[0], world, rank)
     local = forward(images[s:e])
-    return gather_logits(local, images.shape[0], world, group)
+    return gather_logits(local, images.shape[0], world, group, timeout)

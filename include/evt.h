@@ -143,10 +143,26 @@ enum {
   EVT_PROF_FC2 = 6,             /* Dense(D) + LN2(xm) residual          ffn.py:9 */
   EVT_PROF_HEAD = 7,            /* mlp_head / classifier                vit.py:38-39,55 */
   EVT_PROF_QKV_ATTENTION = 8,   /* fused QKV + attention (evt_set_fusion) */
-  EVT_PROF_ROLES = 9
+  EVT_PROF_T2T_UNFOLD = 9,      /* tf_Unfold soft splits 0-2            t2t_vit.py:7-40,66-81 */
+  EVT_PROF_T2T_KQV = 10,        /* TokenPerformer LN1-folded kqv Dense  transformer_encoder.py:84 */
+  EVT_PROF_T2T_PERFORMER = 11,  /* TokenPerformer core (prm_exp .. FFN) transformer_encoder.py:67-99 */
+  EVT_PROF_MERGE = 12,          /* Swin PatchMerging gather + LN-folded reduction */
+  EVT_PROF_ATTN_SUBLAYER = 13,  /* Swin stage-1 fused LN1 + QKV + W-MSA + proj + residual */
+  EVT_PROF_MLP = 14,            /* Swin stage-1 fused LN2 + FC1 + GELU + FC2 + residual */
+  EVT_PROF_ROLES = 15
 };
+/* T2T-ViT also reports its project Dense (+ CLS rows, t2t_vit.py:86,121-125) as PATCH_EMBED and
+ * its LN-folded classifier as HEAD; Swin its patch im2col as PATCHIFY, patch Dense + patch norm
+ * as PATCH_EMBED, W-MSA as ATTENTION, proj as OUT_PROJ, final norm + pool + head as HEAD. */
 int evt_model_profile(evt_model* m, int enable);
 int evt_model_profile_read(evt_model* m, float* us, int* launches);
+/* Algorithmic work of the last profiled forward, per role (arrays of EVT_PROF_ROLES): gflop =
+ * 2 x multiply-adds of the role's contractions (Dense: 2 M K N with the layer's real K, N;
+ * attention: 4 B H N^2 d), gbytes = the bytes its kernels must move at least (every operand read
+ * once, every output written once: activations, weights, residuals, row statistics). Replaces
+ * the reference's FLOP counter (flops_calculation.py:216-251) per kernel; bench.py divides by the
+ * role's time for the MFMA and HBM roofline fractions. */
+int evt_model_profile_work(evt_model* m, double* gflop, double* gbytes);
 
 /* Fused-kernel switches (process-wide; default 0 = the separate QKV GEMM + attention kernels):
  * EVT_FUSE_QKV_ATTENTION runs each bf16 ViT layer's LN1-folded QKV Dense and attention core as

@@ -13,4 +13,4 @@ rc=$?; tail -4 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; rc=$?
 grep -v amdgpu.ids $O/smoke.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --cpu-seconds 3 > $O/bench.log 2>&1 || exit 1
-tail -1 $O/bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['model_roofline']['frac'], d['roofline']['per_role_us'])"
+tail -1 $O/bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['model_roofline']['frac'], {k: (v['us_per_launch'], v['mfma_frac'], v['hbm_frac']) for k, v in d['roofline']['per_role'].items()})"

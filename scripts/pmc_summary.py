@@ -1,6 +1,7 @@
 """Summarise the FETCH_SIZE / WRITE_SIZE passes of scripts/gpu_pmc_fc1.sh for the FC1 probe GEMM
 (the persistent gemm_pers_kernel<35> since the persistent kernel became the default): per-launch HBM bytes, gfx950 FETCH_SIZE doubled (MI355X_MICROARCH.md)."""
 import csv
+import datetime
 import glob
 import json
 import os
@@ -25,5 +26,7 @@ algo = (M * K + K * N + M * N) * 2 if M else None
 print(json.dumps({"kernel": "FC1 LNIN|BIAS|GELU (bf16): " + str(vals.get("kernel_name")), "M": M, "K": K, "N": N,
                   "FETCH_SIZE_KB_raw": vals["FETCH_SIZE"], "WRITE_SIZE_KB": vals["WRITE_SIZE"],
                   "fetch_bytes_corrected": fetch, "write_bytes": write,
-                  "traffic_bytes_per_launch": fetch + write, "algorithmic_bytes": algo},
+                  "traffic_bytes_per_launch": fetch + write, "algorithmic_bytes": algo,
+                  "commit": os.environ.get("COMMIT"),
+                  "collected": datetime.datetime.utcnow().strftime("%Y-%m-%dT%H:%MZ")},
                  indent=1))
