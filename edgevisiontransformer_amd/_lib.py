@@ -27,7 +27,7 @@ DTYPE = {"f32": 0, "fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1, "mx8": 2}
 EPI_BIAS, EPI_GELU, EPI_RESID, EPI_POS, EPI_OUT_F32 = 1, 2, 4, 8, 16
 EPI_LNIN, EPI_RESLN, EPI_STATS, EPI_GELU_ERF = 32, 64, 128, 256
 EPI_OUT_MX8 = 512
-FUSE_QKV_ATTENTION = 1  # evt_set_fusion flag (include/evt.h EVT_FUSE_QKV_ATTENTION)
+FUSE_QKV_ATTENTION = 1  # evt_model_set_fusion flag (include/evt.h EVT_FUSE_QKV_ATTENTION)
 # evt_model_profile roles (include/evt.h EVT_PROF_*)
 PROF_ROLES = ("patchify", "patch_embed", "qkv", "attention", "out_proj", "fc1", "fc2", "head",
               "qkv_attention", "t2t_unfold", "t2t_kqv", "t2t_performer", "merge", "attn_sublayer",
@@ -112,7 +112,7 @@ SIGNATURES = {
     "evt_graph_capture": (_I, [_P, _P, _I, _P, _P]),
     "evt_graph_launch": (_I, [_P, _P]),
     "evt_set_gemm_variant": (_I, [_I]),
-    "evt_set_fusion": (_I, [_I]),
+    "evt_model_set_fusion": (_I, [_P, _I]),
     "evt_model_profile": (_I, [_P, _I]),
     "evt_model_profile_read": (_I, [_P, _P, _P]),
     "evt_model_profile_work": (_I, [_P, _P, _P]),
@@ -120,6 +120,7 @@ SIGNATURES = {
     "evt_pack_weight": (_I, [_I, _P, _P, _I, _I, _P, _I, _I, _P]),
     "evt_ln_fold": (_I, [_I, _P, _I, _I, _P, _P, _P, _I, _I, _P, _P, _P]),
     "evt_dense": (_I, [_I, ctypes.POINTER(evt_dense_args), _P]),
+    "evt_dense_splitk": (_I, [_I, ctypes.POINTER(evt_dense_args), _I, _P, _P]),
     "evt_attention": (_I, [_I, _P, _I64, _P, _I64, _I, _I, _I, _F, _P]),
     "evt_layernorm": (_I, [_I, _P, _I64, _P, _I64, _P, _P, _I, _I, _F, _P]),
     "evt_patchify": (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P]),

@@ -12,14 +12,20 @@ from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-LIB = os.path.join(HERE, "libevt_hip.so")
-OBJ = os.path.join(HERE, "build_obj")
+# EVT_LAB=1: the diagnostic build (GEMM ablation / timeline variants, qkv_attn ablations) into
+# libevt_hip_lab.so (load it with EVT_LIB=<path>); the product library never contains them
+LAB = os.environ.get("EVT_LAB", "") not in ("", "0")
+LIB = os.path.join(HERE, "libevt_hip_lab.so" if LAB else "libevt_hip.so")
+OBJ = os.path.join(HERE, "build_obj_lab" if LAB else "build_obj")
 SOURCES = ["gemm.hip", "attention.hip", "qkv_attn.hip", "norm.hip", "t2t.hip", "swin.hip", "mx8.hip", "capi.cpp"]
 HEADERS = ["common.h", "evt_internal.h", os.path.join("..", "..", "include", "evt.h")]
 ARCH = os.environ.get("EVT_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
          "-ffp-contract=on"]  # contraction only within one source expression: same result on
 #                                every code path (interior / edge tiles) -> batch-independent bits
+if LAB:
+    FLAGS += ["-DEVT_GEMM_LAB"] + ([f"-DEVT_QA_DBG={os.environ['EVT_QA_DBG']}"]
+                                   if os.environ.get("EVT_QA_DBG") else [])
 
 
 # MFMA results straight into VGPRs: with the default AGPR form the compiler parks the small

@@ -153,6 +153,7 @@ struct evt_model {
   hipGraph_t graph = nullptr;        // evt_graph_capture
   hipGraphExec_t graph_exec = nullptr;
   // evt_model_profile: HIP events around every launch of the last forward, by role
+  int fusion = 0;                    // evt_model_set_fusion (opt-in)
   bool prof = false;
   std::vector<hipEvent_t> prof_ev;   // pool (pairs)
   std::vector<int> prof_role;        // role of pair i of the last forward
@@ -162,8 +163,6 @@ struct evt_model {
 
 namespace {
 
-int g_fusion = 0;  // evt_set_fusion (opt-in: the fused kernel is slower today)
-bool fused_attention_enabled() { return (g_fusion & EVT_FUSE_QKV_ATTENTION) != 0; }
 
 // evt_model_profile: a pair of events around each launch of a forward (profiling forwards only)
 struct ProfScope {
@@ -483,7 +482,7 @@ int alloc_encoder_ws(evt_model* m, int B, size_t hbuf_bytes, hipStream_t s) {
 int dense_head(const evt_model* m, const DenseW& w, const DenseCall& c, hipStream_t s) {
   const int tiles = ((c.M + GEMM_BM - 1) / GEMM_BM) * (w.npad / GEMM_BN);
   int S = 1;
-  while (S < 8 && tiles * S * 2 <= 256 && w.kpad % (S * 2 * PAD_K) == 0) S *= 2;
+  while (S < 8 && tiles * S * 2 <= device_cus() && w.kpad % (S * 2 * PAD_K) == 0) S *= 2;
   const size_t part = (size_t)S * c.M * w.npad * sizeof(float);
   if (S < 2 || !m->hbuf || part > m->hbuf_bytes ||
       (c.flags & ~(EPI_BIAS | EPI_GELU | EPI_OUT_F32)))
@@ -501,7 +500,7 @@ int run_encoder(evt_model* m, int B, hipStream_t s) {
   const int D = m->D, T = m->sh.T, rows = B * T;
   const float log2e = 1.4426950408889634f;
   const bool fuse = m->dtype == DT_BF16 && D % 64 == 0 && qkv_attn_supported(T, D) &&
-                    fused_attention_enabled();
+                    (m->fusion & EVT_FUSE_QKV_ATTENTION) != 0;
   for (const Layer& L : m->layers) {
     if (fuse) {  // LN1-folded QKV + attention in one kernel (qkv_attn.hip)
       ProfScope ps(m, EVT_PROF_QKV_ATTENTION, s);
@@ -1442,16 +1441,17 @@ int evt_patch_merge(int dtype, const void* x, int64_t ldx, int B, int R, int C, 
 
 // ---- op-level entry points --------------------------------------------------------------
 
-int evt_set_fusion(int flags) {
+int evt_model_set_fusion(evt_model* m, int flags) {
+  if (!m) return fail(EVT_EINVAL, "model is NULL");
   if (flags & ~EVT_FUSE_QKV_ATTENTION) return fail(EVT_EINVAL, "unknown fusion flag");
-  g_fusion = flags;
+  m->fusion = flags;
   return EVT_OK;
 }
 
 int evt_set_gemm_variant(int variant) {
-  if (variant != 0 && variant != 1 && variant != 2 && variant != 6 && variant != 8 &&
-      !(variant >= 9 && variant <= 25) && variant != 106 && variant != 108)
-    return fail(EVT_EINVAL, "variant must be 0, 1, 2, 6, 8, 9-23, 106 or 108");
+  if (!gemm_variant_supported(variant))
+    return fail(EVT_EINVAL, "variant must be 0, 1, 2, 6, 8, 9 or 16 (lab builds: also 10, 11, 13, "
+                            "15, 17-25, 106, 108)");
   gemm_set_variant(variant);
   return EVT_OK;
 }
@@ -1594,6 +1594,25 @@ int evt_dense(int dtype, const evt_dense_args* a, void* stream) {
   hipError_t e = gemm_launch(dtype, f, p, (hipStream_t)stream);
   if (e == hipErrorInvalidValue) return fail(EVT_EINVAL, "dense: unsupported flags/shape");
   EVT_HIP(e, "dense");
+  return EVT_OK;
+}
+
+int evt_dense_splitk(int dtype, const evt_dense_args* a, int splits, float* partials,
+                     void* stream) {
+  if (!a || !a->A || !a->Wp || !a->C || !partials || a->M < 0 || a->N <= 0 || a->N > a->Npad ||
+      a->Kpad % PAD_K || a->Npad % GEMM_BN || a->lda < a->Kpad || a->ldc < a->N)
+    return fail(EVT_EINVAL, "dense_splitk: bad shape");
+  if (a->flags & ~(EPI_BIAS | EPI_GELU | EPI_OUT_F32))
+    return fail(EVT_EINVAL, "dense_splitk: flags must be a subset of BIAS | GELU | OUT_F32");
+  if ((a->flags & EPI_BIAS) && !a->bias) return fail(EVT_EINVAL, "dense_splitk: bias flag without bias");
+  if (splits < 1 || splits > 64 || a->Kpad % (splits * PAD_K))
+    return fail(EVT_EINVAL, "dense_splitk: Kpad must be a multiple of splits * 64");
+  GemmParams p{};
+  p.A = a->A; p.lda = a->lda; p.W = a->Wp; p.ldw = a->Kpad; p.C = a->C; p.ldc = a->ldc;
+  p.M = a->M; p.N = a->N; p.K = a->Kpad; p.ntiles = a->Npad / GEMM_BN; p.bias = a->bias;
+  hipError_t e = gemm_splitk_launch(dtype, a->flags, p, splits, partials, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue) return fail(EVT_EINVAL, "dense_splitk: unsupported flags/shape");
+  EVT_HIP(e, "dense_splitk");
   return EVT_OK;
 }
 

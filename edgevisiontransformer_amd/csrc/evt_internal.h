@@ -61,6 +61,7 @@ hipError_t gemm_launch(int dtype, int flags, const GemmParams& p, hipStream_t s)
 // Skinny GEMM (small M, long K: the classifier head) as S K-splits in one launch, fp32 partials
 // part[S][M][ntiles*128], then a fixed-order reduction + bias (+ GELU) into C (deterministic).
 // flags: EPI_BIAS and/or EPI_GELU and/or EPI_OUT_F32 only; K % (S * 64) == 0.
+int device_cus();  // compute units of the current device (cached)
 hipError_t gemm_splitk_launch(int dtype, int flags, const GemmParams& p, int S, float* part,
                               hipStream_t s);
 void gemm_set_variant(int v);
@@ -106,7 +107,7 @@ struct QkvAttnParams {
   int H, N, B;
   void* out; int64_t ldo;
   float scale_log2;
-  int dbg;        // diagnostic ablations (EVT_QA_DBG): 1 no attention, 2 main loop only,
+  int dbg;        // lab-build ablations (-DEVT_QA_DBG=n): 1 no attention, 2 main loop only,
                   // 3 one workgroup per CU
 };
 bool qkv_attn_supported(int N, int K);
@@ -214,7 +215,8 @@ struct SwinAttnBlockParams {
   float eps;
 };
 hipError_t swin_attn96_launch(const SwinAttnBlockParams& p, hipStream_t s);
-int gemm_variant();  // the process-wide evt_set_gemm_variant value (0 = automatic)
+int gemm_variant();  // the calling thread's evt_set_gemm_variant value (0 = automatic)
+bool gemm_variant_supported(int v);  // compiled into this build (lab variants: EVT_GEMM_LAB)
 
 // ---- MXFP8 (mx8.hip): e4m3fn elements, e8m0 scale per 32 K, scales S[K/128][ld] dwords ----
 struct Mx8GemmParams {

@@ -492,7 +492,11 @@ constexpr int BIG_BM = 256, BIG_BN = 256;
 constexpr int BIG_TILE = BIG_BM * ROWB;       // 32 KiB per operand
 constexpr int BIG_STAGE = 2 * BIG_TILE;       // 64 KiB per K-tile
 
-int g_gemm_variant = 0;  // 0 auto, 1 force 128x128, 2 / 6 256x256 VAR 0 / 6
+// evt_set_gemm_variant, per calling thread (launch decisions are made on the launching thread):
+// 0 auto, 1 force 128x128, 2 / 6 / 8 non-persistent 256x256 main loops, 9 tile-persistent,
+// 16 stream-K. Lab builds (-DEVT_GEMM_LAB) add the ablation / timeline / A-B variants 10, 11, 13,
+// 15, 17-25, 106, 108 used by scripts/gemm_bench.py and scripts/probe/pers_timeline.py.
+thread_local int g_gemm_variant = 0;
 
 bool use_big(const GemmParams& p, int flags) {
   if ((p.ntiles * GEMM_BN) % BIG_BN) return false;
@@ -1707,10 +1711,12 @@ hipError_t launch_big(const GemmParams& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_big_kernel<FL, 0>), grid, dim3(512), 0, s, q);
   else if (g_gemm_variant == 8)
     hipLaunchKernelGGL((gemm_big_kernel<FL, 8>), grid, dim3(512), 0, s, q);
+#ifdef EVT_GEMM_LAB
   else if (g_gemm_variant == 106)
     hipLaunchKernelGGL((gemm_big_kernel<FL, 6, true>), grid, dim3(512), 0, s, q);
   else if (g_gemm_variant == 108)
     hipLaunchKernelGGL((gemm_big_kernel<FL, 8, true>), grid, dim3(512), 0, s, q);
+#endif
   else if constexpr ((FL & EPI_POS) != 0)  // patch embedding: 8-phase loop (153 vs 179 us, bs512)
     hipLaunchKernelGGL((gemm_big_kernel<FL, 8>), grid, dim3(512), 0, s, q);
   else
@@ -1740,10 +1746,20 @@ constexpr bool pers_fl(int fl) {
 }
 
 // persistent kernel: supported epilogue, 8-column output groups, LN rows of <= 8 slots
+bool gemm_lab_pers_variant(int v) {
+#ifdef EVT_GEMM_LAB
+  return v == 10 || v == 11 || v == 13 || v == 15 || (v >= 17 && v <= 25);
+#else
+  (void)v;
+  return false;
+#endif
+}
+
 bool use_pers(const GemmParams& p, int flags) {
-  if (g_gemm_variant != 0 && (g_gemm_variant < 9 || g_gemm_variant > 25 || g_gemm_variant == 12 ||
-                              g_gemm_variant == 14))
-    return false;
+  const int v = g_gemm_variant;
+  if (v != 0 && v != 9 && v != 16 && !gemm_lab_pers_variant(v)) return false;
+  // timeline variants stamp s_memtime through p.pos: never on the patch GEMM (p.pos = the table)
+  if ((v == 13 || v == 15) && (flags & EPI_POS)) return false;
   if (p.N % 8 || p.vec_ok < 2) return false;
   if ((flags & (EPI_LNIN | EPI_RESLN)) && (p.nslots > 8 || p.nslots % 2 || p.stats_step > 1))
     return false;
@@ -1760,9 +1776,12 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
   const int total = ((p.M + BIG_BM - 1) / BIG_BM) * q.ntiles;
   int G = min(total, g_gemm_variant == 10 ? 8 : g_num_cus);  // 10: few blocks, many tiles each
   if (G >= 8) G &= ~7;
-  if (g_gemm_variant == 11)
+  if (false) {
+  }
+#ifdef EVT_GEMM_LAB
+  else if (g_gemm_variant == 11)
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 1>), dim3(G), dim3(512), 0, s, q, total);
-  else if (g_gemm_variant == 13)  // timeline probe: p.pos = u64 [blocks][16][4]
+  else if (g_gemm_variant == 13)  // timeline probe: p.pos = u64 [blocks][16][8]
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 3>), dim3(G), dim3(512), 0, s, q, total);
   else if (g_gemm_variant == 15)  // timeline probe + staggered block start
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 5>), dim3(G), dim3(512), 0, s, q, total);
@@ -1785,6 +1804,7 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
   else if (g_gemm_variant == 18)  // ablation: epilogue without the GELU
     hipLaunchKernelGGL((gemm_pers_kernel<(FL & ~(EPI_GELU | EPI_GELU_ERF)), 0, false>), dim3(G),
                        dim3(512), 0, s, q, total);
+#endif
   else if (p.N % BIG_BN == 0)
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 0, false>), dim3(G), dim3(512), 0, s, q, total);
   else
@@ -1950,7 +1970,16 @@ __global__ void fold_kernel(const T* __restrict__ Wp, int Kpad, const float* __r
 
 }  // namespace
 
+int device_cus() { return num_cus(); }
 void gemm_set_variant(int v) { g_gemm_variant = v; }
+bool gemm_variant_supported(int v) {
+  return v == 0 || v == 1 || v == 2 || v == 6 || v == 8 || v == 9 || v == 16 ||
+         gemm_lab_pers_variant(v)
+#ifdef EVT_GEMM_LAB
+         || v == 106 || v == 108
+#endif
+      ;
+}
 int gemm_variant() { return g_gemm_variant; }
 
 size_t gemm_sk_bytes() { return 4096 + (size_t)SK_MAX_G * SK_SLOT_FLOATS * sizeof(float); }

@@ -119,14 +119,7 @@ int evt_model_destroy(evt_model* model);
 
 /* ---- op-level entry points (one per hot-path kernel; used by the parity tests) ---------- */
 
-/* GEMM tile-shape policy for bf16 (process-wide tuning knob): 0 = automatic (256x256 tiles when
- * the problem has >= 256 of them, else 128x128; among 256x256 GEMMs with a fused epilogue the
- * stream-K persistent kernel when there are at least #CUs tiles, else the tile-persistent one),
- * 1 = always 128x128, 2 / 6 / 8 = 256x256 tiles with the plain / interleaved / 8-phase ping-pong
- * main loop whenever the packed width allows (and the output rows are 16-B aligned for bf16),
- * 9 = tile-persistent kernel (no stream-K), 16 = stream-K where it applies; 10-15, 17-19 and 106 / 108
- * are diagnostic builds (timeline stamps, main loop only). */
-int evt_set_gemm_variant(int variant);
+
 
 /* Per-kernel timing of real forwards (the reference times whole models and per-layer micro-models,
  * tools.py:82-116 / utils.py:322-406; this is the device-side equivalent): while enabled, every
@@ -142,7 +135,7 @@ enum {
   EVT_PROF_FC1 = 5,             /* LN2-folded Dense(M, gelu)            ffn.py:8 */
   EVT_PROF_FC2 = 6,             /* Dense(D) + LN2(xm) residual          ffn.py:9 */
   EVT_PROF_HEAD = 7,            /* mlp_head / classifier                vit.py:38-39,55 */
-  EVT_PROF_QKV_ATTENTION = 8,   /* fused QKV + attention (evt_set_fusion) */
+  EVT_PROF_QKV_ATTENTION = 8,   /* fused QKV + attention (evt_model_set_fusion) */
   EVT_PROF_T2T_UNFOLD = 9,      /* tf_Unfold soft splits 0-2            t2t_vit.py:7-40,66-81 */
   EVT_PROF_T2T_KQV = 10,        /* TokenPerformer LN1-folded kqv Dense  transformer_encoder.py:84 */
   EVT_PROF_T2T_PERFORMER = 11,  /* TokenPerformer core (prm_exp .. FFN) transformer_encoder.py:67-99 */
@@ -164,12 +157,13 @@ int evt_model_profile_read(evt_model* m, float* us, int* launches);
  * role's time for the MFMA and HBM roofline fractions. */
 int evt_model_profile_work(evt_model* m, double* gflop, double* gbytes);
 
-/* Fused-kernel switches (process-wide; default 0 = the separate QKV GEMM + attention kernels):
- * EVT_FUSE_QKV_ATTENTION runs each bf16 ViT layer's LN1-folded QKV Dense and attention core as
- * one kernel (evt_qkv_attention) where the token count allows. Opt-in: measured slower than the
- * separate kernels at DeiT-base bs512 ("Fused QKV + attention"). */
+/* Fused-kernel switches of ONE model handle (default 0 = the separate QKV GEMM + attention
+ * kernels): EVT_FUSE_QKV_ATTENTION runs each bf16 ViT layer's LN1-folded QKV Dense and attention
+ * core as one kernel (evt_qkv_attention) where the token count allows. Opt-in: measured slower
+ * than the separate kernels at DeiT-base bs512 ("Fused QKV + attention"). Takes effect
+ * at the next forward / graph capture of that handle; other handles are unaffected. */
 #define EVT_FUSE_QKV_ATTENTION 1
-int evt_set_fusion(int flags);
+int evt_model_set_fusion(evt_model* m, int flags);
 
 /* Pack a Keras [K, N] fp32 kernel into the GEMM operand layout Wp[Npad][Kpad] (dtype), zero
  * padded, optionally scaling row k by row_scale[k] (a LayerNorm gamma folded into the weights;
@@ -222,6 +216,14 @@ typedef struct evt_dense_args {
  * residual + stats); Swin: 289 (LN-folded FC1 + erf GELU), 133 (proj / FC2 + residual + stats),
  * 161 (LN-folded patch-merge reduction + stats). */
 int evt_dense(int dtype, const evt_dense_args* args, void* stream);
+
+/* The same Dense as `splits` K-slices in one launch (the classifier head's path, M = batch: the
+ * plain tile grid would leave most CUs idle): fp32 partial products into `partials`
+ * ([splits][M][Npad] floats, caller-owned), then a fixed-order reduction with bias / tanh GELU
+ * (flags a subset of EVT_EPI_BIAS | EVT_EPI_GELU | EVT_EPI_OUT_F32; Kpad % (splits * 64) == 0).
+ * Reference: mlp_head `vit.py:38-39,55`. */
+int evt_dense_splitk(int dtype, const evt_dense_args* args, int splits, float* partials,
+                     void* stream);
 
 /* Fused attention sublayer up to the out-projection (bf16 only): the LN1-folded QKV Dense
  * (norm.py:12 + attention.py:17,24) and the attention core (attention.py:20-34) in one kernel, q / k
@@ -430,6 +432,18 @@ int evt_mx8_layernorm(const void* x, int rows, int D, int Kpad, const float* gam
  * MX8 model's out-proj operand (attention.py:20-35). ldq8 % 128 == 0, ldq8 >= 64*H. */
 int evt_attention_mx8(const void* qkv, int64_t ldq, void* q8, int64_t ldq8, uint32_t* s8,
                       int64_t ld_s8, int B, int N, int H, float scale, void* stream);
+
+/* ---- diagnostics (not part of the model contract) ---------------------------------------- */
+
+/* GEMM kernel selection for bf16 Dense launches made FROM THE CALLING THREAD (thread-local: other
+ * threads and their handles are unaffected), for parity tests and A/B measurements only:
+ * 0 = automatic (256x256 tiles when the problem has >= 256 of them, the tile-persistent kernel
+ * for the fused epilogues, else 128x128), 1 = always 128x128, 2 / 6 / 8 = non-persistent 256x256
+ * tiles with the plain / interleaved / 8-phase ping-pong main loop whenever the packed width
+ * allows, 9 = tile-persistent, 16 = stream-K persistent where it applies. Builds with
+ * EVT_LAB=1 (-DEVT_GEMM_LAB) also accept the ablation / timeline variants 10, 11, 13, 15, 17-25,
+ * 106, 108; other values return EVT_EINVAL. */
+int evt_set_gemm_variant(int variant);
 
 #ifdef __cplusplus
 }

@@ -1,5 +1,7 @@
 """GEMM microbenchmark on the GPU: model-shaped bf16 GEMMs, 128x128 vs 256x256 tile kernels,
-interleaved rounds in one process (HIP events), plus a cross-check of the two variants."""
+interleaved rounds in one process (HIP events), plus a cross-check of the two variants.
+Ablation / A-B variants (10, 11, 13, 15, 17-25, 106, 108) exist only in the lab build:
+  EVT_LAB=1 python -m edgevisiontransformer_amd.build && EVT_LIB=edgevisiontransformer_amd/libevt_hip_lab.so python scripts/gemm_bench.py ..."""
 import ctypes
 import json
 import sys

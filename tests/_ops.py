@@ -64,6 +64,21 @@ def dense(dtype, flags, A, wp, kpad, npad, M, N, ldc=None, bias=None, resid=None
     return C
 
 
+def dense_splitk(dtype, flags, A, wp, kpad, npad, M, N, splits, bias=None, C=None):
+    """evt_dense_splitk: the classifier head's K-split Dense (fp32 partials, fixed-order reduce)."""
+    out_f32 = bool(flags & _lib.EPI_OUT_F32)
+    if C is None:
+        C = torch.zeros((M, N), dtype=torch.float32 if out_f32 else TDT[dtype], device=A.device)
+    part = torch.full((splits, M, npad), float("nan"), device=A.device)
+    a = _lib.evt_dense_args()
+    a.flags, a.A, a.lda, a.Wp, a.Kpad, a.Npad = flags, A.data_ptr(), A.stride(0), wp.data_ptr(), kpad, npad
+    a.C, a.ldc, a.M, a.N = C.data_ptr(), C.stride(0), M, N
+    a.bias = bias.data_ptr() if bias is not None else None
+    _lib.check(_lib.load_library().evt_dense_splitk(_lib.DTYPE[dtype], ctypes.byref(a), splits,
+                                                     _p(part), _s()))
+    return C
+
+
 def attention(dtype, qkv, B, N, H, scale=0.125, out=None):
     if out is None:
         out = torch.zeros((B * N, H * 64), dtype=TDT[dtype], device=qkv.device)

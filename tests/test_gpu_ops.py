@@ -80,6 +80,38 @@ def _dense_case(gpu, dtype, M, K, N, flags):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("M,K,N", [(1, 768, 3072), (37, 3072, 1000), (130, 768, 148), (257, 1536, 200)])
+@pytest.mark.parametrize("flags", [_lib.EPI_BIAS | _lib.EPI_GELU, _lib.EPI_BIAS | _lib.EPI_OUT_F32,
+                                   _lib.EPI_BIAS | _lib.EPI_GELU | _lib.EPI_OUT_F32])
+@pytest.mark.parametrize("splits", [2, 4, 8])
+def test_dense_splitk(gpu, dtype, M, K, N, flags, splits):
+    """evt_dense_splitk (the classifier head path, vit.py:38-39,55): S K-slices with fp32 partials
+    and a fixed-order reduce + bias / GELU, against the plain Dense on the same operands (the only
+    difference is the fp32 summation order: within one output rounding) and an fp64 reference;
+    M edges (1, 37, 130, 257 rows) and N not a multiple of the 128-column tile."""
+    if K % (splits * 64):
+        pytest.skip("Kpad must be a multiple of splits * 64")
+    A64, W64, b64 = _rand((M, K), 31), _rand((K, N), 32, 1 / math.sqrt(K)), _rand((N,), 33, 0.1)
+    A = A64.to(_ops.TDT[dtype]).to(gpu)
+    wp, kpad, npad = _ops.pack(W64.float().to(gpu), dtype)
+    bias = torch.zeros(npad, device=gpu)
+    bias[:N] = b64.float().to(gpu)
+    got = _ops.dense_splitk(dtype, flags, A, wp, kpad, npad, M, N, splits, bias=bias)
+    plain = _ops.dense(dtype, flags, A, wp, kpad, npad, M, N, bias=bias)
+    torch.cuda.synchronize()
+    ref = _q(A64, dtype) @ _q(W64.float().double(), dtype) + b64.float().double()
+    if flags & _lib.EPI_GELU:
+        ref = _gelu(ref)
+    out_f32 = bool(flags & _lib.EPI_OUT_F32)
+    tol = TOL["f32"] if dtype == "f32" or out_f32 else TOL["bf16"]
+    if dtype == "bf16" and out_f32:
+        tol = dict(rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(got.double().cpu(), ref, **tol)
+    same = dict(rtol=1e-5, atol=1e-5) if out_f32 or dtype == "f32" else dict(rtol=8e-3, atol=8e-3)
+    torch.testing.assert_close(got.float(), plain.float(), **same)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
 def test_dense_patch_embed_remap(gpu, dtype):
     B, P, K, N = 3, 196, 768, 192
     A64, W64, b64 = _rand((B * P, K), 5), _rand((K, N), 6, 1 / 28.0), _rand((N,), 7, 0.1)

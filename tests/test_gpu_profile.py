@@ -18,16 +18,12 @@ def test_profile_roles_deit_tiny(gpu, fusion):
     m = build_named("deit_tiny", dtype="bf16", seed=0, max_batch=8)
     img = torch.randn((8, 3, 224, 224), device=gpu)
     logits = torch.empty((8, 1000), device=gpu)
-    lib = _lib.load_library()
-    lib.evt_set_fusion(fusion)
-    try:
-        kernel_times(m, img, logits, forwards=1)  # warm-up (event pool)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        kt = kernel_times(m, img, logits, forwards=3)
-        wall_us = (time.perf_counter() - t0) / 3 * 1e6  # per profiled forward (+ one extra)
-    finally:
-        lib.evt_set_fusion(0)
+    m.set_fusion(fusion)
+    kernel_times(m, img, logits, forwards=1)  # warm-up (event pool)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kt = kernel_times(m, img, logits, forwards=3)
+    wall_us = (time.perf_counter() - t0) / 3 * 1e6  # per profiled forward (+ one extra)
     expect = {"patchify": 1, "patch_embed": 1, "out_proj": 12, "fc1": 12, "fc2": 12, "head": 1}
     if fusion:
         expect["qkv_attention"] = 12
