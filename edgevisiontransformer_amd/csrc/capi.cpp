@@ -885,22 +885,6 @@ int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* 
   const int D = d.dim, T = sh.T, dt = m->dtype;
   prof_reset(m);
   // patch embedding (vit.py:45-51): rearrange -> Dense(D) + pos, CLS row = cls + pos[0]
-  if (m->patch_cm && dt == DT_BF16 && d.patch_size == 16 && !m->mx8 && gemm_variant() == 0) {
-    // the patch gather inside the GEMM's A loader: no patch matrix in HBM
-    ProfScope ps(m, EVT_PROF_PATCH_EMBED, s);
-    const int M = B * sh.P;
-    prof_work(m, 2.0 * M * sh.pd * D,
-              (double)B * d.in_chans * d.image_size * d.image_size * 4 + (double)sh.pd * D * 2 +
-                  (double)B * T * D * 2 + (double)B * T * stats_slots(D) * 8 + (double)T * D * 4);
-    EVT_HIP(cls_rows_launch(dt, m->x, B, T, D, m->cls, m->pos, m->sx, s), "cls rows");
-    GemmParams p{};
-    p.W = m->patch.w; p.ldw = m->patch.kpad; p.C = m->x; p.ldc = D;
-    p.M = M; p.N = D; p.K = m->patch.kpad; p.ntiles = m->patch.npad / GEMM_BN;
-    p.bias = m->patch.b; p.pos = m->pos; p.ldp = D; p.P = sh.P;
-    p.vec_ok = (D % 8 == 0) ? 2 : (D % 4 == 0);
-    p.stats_out = m->sx; p.inv_d = 1.0f / (float)D; p.eps = m->eps; p.nslots = stats_slots(D);
-    EVT_HIP(patch_gemm_launch(p, img, d.in_chans, d.image_size, s), "patch embed (fused gather)");
-  } else {
   {
     ProfScope ps(m, EVT_PROF_PATCHIFY, s);
     prof_work(m, 0.0, (double)B * d.in_chans * d.image_size * d.image_size * 4 +
@@ -918,7 +902,6 @@ int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* 
     c.pos = m->pos; c.ldp = D; c.P = sh.P; c.stats_out = m->sx;
     c.resid = m->pos_h; c.ldr = m->pos_h ? D : 0;  // bf16 table for the persistent kernel
     EVT_RC(dense(m, m->patch, c, s));
-  }
   }
   EVT_RC(m->mx8 ? run_encoder_mx8(m, B, s) : run_encoder(m, B, s));
   ProfScope ps_head(m, EVT_PROF_HEAD, s);

@@ -62,10 +62,6 @@ hipError_t gemm_launch(int dtype, int flags, const GemmParams& p, hipStream_t s)
 // part[S][M][ntiles*128], then a fixed-order reduction + bias (+ GELU) into C (deterministic).
 // flags: EPI_BIAS and/or EPI_GELU and/or EPI_OUT_F32 only; K % (S * 64) == 0.
 int device_cus();  // compute units of the current device (cached)
-// bf16 patch embedding with the patch gather in the A loader (gemm.hip patch_gemm_kernel): rows
-// m = b P + t of the NCHW fp32 image `img` (C channels, HW x HW, patch 16, channel-major K, W packed
-// from patch_weight_cm), flags EPI_BIAS | EPI_POS | EPI_STATS; p.A unused.
-hipError_t patch_gemm_launch(const GemmParams& p, const float* img, int C, int HW, hipStream_t s);
 hipError_t gemm_splitk_launch(int dtype, int flags, const GemmParams& p, int S, float* part,
                               hipStream_t s);
 void gemm_set_variant(int v);

@@ -480,129 +480,6 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmParams p) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Patch embedding with the patch gather in the A loader (reference
-// `vit.py:31-32,45-46`: Rearrange + Dense): no patch matrix in HBM. The 128x128 tile of
-// gemm_nt_kernel (4 waves, 64x64 each, two blocks per CU) with A row m = patch (b, t) of the NCHW
-// fp32 image and K in the channel-major order k = c*256 + p1*16 + p2 of patch_weight_cm (ps = 16):
-// K-tile kt is channel kt/4, image rows 4 (kt % 4) .. +3 of the patch, 16 pixels each, i.e. four
-// 64-B runs per A row. Each thread owns 4 LDS chunks (8 K values) per K-tile: two 16-B fp32
-// loads per chunk issued one K-tile ahead into registers, converted to bf16 and written to the
-// swizzled LDS image after the current K-tile's MFMAs (W arrives by glds as usual). Epilogue as
-// gemm_nt_kernel (EPI_BIAS | EPI_POS | EPI_STATS: + pos[t+1], rows remapped past the CLS rows).
-// ---------------------------------------------------------------------------------------------
-template <int FL>
-__global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmParams p, const float* __restrict__ img,
-                                                            int C, int HW) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave & 1, wn = wave >> 1;
-  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = wgid / p.ntiles, tn = wgid - tm * p.ntiles;
-  const int m0 = tm * GEMM_BM, n0 = tn * GEMM_BN;
-  const int np = HW >> 4;
-
-  // A chunks of this thread: e = q * 256 + tid -> tile row r = e >> 3, logical chunk L = e & 7
-  // (image row p1 = 4 (kt % 4) + (L >> 1), pixels (L & 1) * 8 .. + 7 of the patch's 16)
-  int abase[4];
-  int aoff[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int e = q * 256 + tid, r = e >> 3, L = e & 7;
-    const int m = min(m0 + r, p.M - 1);
-    const int b = m / p.P, t = m - b * p.P, hh = t / np, ww = t - hh * np;
-    abase[q] = ((b * C) * HW + hh * 16 + (L >> 1)) * HW + ww * 16 + (L & 1) * 8;
-    aoff[q] = r * ROWB + ((L ^ (r & 7)) << 4);
-  }
-  f32x4 areg[4][2];
-  auto loadA = [&](int kt) {
-    const int koff = ((kt >> 2) * HW + (kt & 3) * 4) * HW;  // channel, image-row block
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float* src = img + abase[q] + koff;
-      areg[q][0] = *(const f32x4*)src;
-      areg[q][1] = *(const f32x4*)(src + 4);
-    }
-  };
-  auto writeA = [&](int buf) {
-    EVT_LDS char* base = (EVT_LDS char*)smem + buf * STAGE_BYTES;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const bf16x8 o = {(bf16)areg[q][0][0], (bf16)areg[q][0][1], (bf16)areg[q][0][2],
-                        (bf16)areg[q][0][3], (bf16)areg[q][1][0], (bf16)areg[q][1][1],
-                        (bf16)areg[q][1][2], (bf16)areg[q][1][3]};
-      *(EVT_LDS bf16x8*)(base + aoff[q]) = o;
-    }
-  };
-  // W rows [wave*32, wave*32+32) of the tile by glds (as gemm_nt_kernel)
-  const int srow = lane >> 3, sslot = lane & 7;
-  const int64_t ldw_b = p.ldw * (int64_t)sizeof(bf16);
-  const char* w_base = (const char*)p.W + (int64_t)(n0 + wave * 32 + srow) * ldw_b + ((sslot ^ srow) * 16);
-  auto stageW = [&](int kt, int buf) {
-    EVT_LDS char* base = (EVT_LDS char*)smem + buf * STAGE_BYTES + TILE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      glds16(w_base + (i * 8) * ldw_b + (int64_t)kt * ROWB, base + (wave * 32 + i * 8) * ROWB);
-  };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = p.K / 64;
-  loadA(0);
-  stageW(0, 0);
-  wait_vmcnt0();
-  writeA(0);
-  const int frow = lane & 15, fsw = lane & 7, fg = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    __syncthreads();  // buffer kt & 1 complete (ds_writes + DMA); buffer (kt+1) & 1 free
-    const bool more = kt + 1 < nk;
-    if (more) {
-      loadA(kt + 1);
-      stageW(kt + 1, (kt + 1) & 1);
-    }
-    const EVT_LDS char* As = (const EVT_LDS char*)smem + (kt & 1) * STAGE_BYTES;
-    const EVT_LDS char* Ws = As + TILE_BYTES;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int coff = ((fg + 4 * kk) ^ fsw) * 16;
-      u32x4 a[4], w[4];
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        a[mt] = *(const EVT_LDS u32x4*)(As + (wm * 64 + mt * 16 + frow) * ROWB + coff);
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-        w[nt] = *(const EVT_LDS u32x4*)(Ws + (wn * 64 + nt * 16 + frow) * ROWB + coff);
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) Mma<bf16>::run(w[nt], a[mt], acc[nt][mt]);
-    }
-    if (more) {
-      wait_vmcnt0();
-      writeA((kt + 1) & 1);
-    }
-  }
-
-  __syncthreads();
-  EVT_LDS char* stg = (EVT_LDS char*)smem;
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const int row = wm * 64 + mt * 16 + frow;
-      *(EVT_LDS f32x4*)(stg + stg_off(row, wn * 16 + nt * 4 + fg)) = acc[nt][mt];
-    }
-  __syncthreads();
-  const bool interior = p.vec_ok && (n0 + GEMM_BN <= p.N) && (m0 + GEMM_BM <= p.M);
-  epi_rows<bf16, FL>(p, stg, m0, n0 + (lane & 31) * 4, n0 + (lane & 15) * 8, wave * 32, lane,
-                     n0 / 128, interior);
-}
-
-// ---------------------------------------------------------------------------------------------
 // Large-tile bf16 kernel: 256x256 output tile, BK = 64, 512 threads = 8 waves in 2 (m) x 4 (n),
 // each wave a 128 (m) x 64 (n) sub-tile = 8 x 4 MFMA tiles (128 fp32 accumulators per lane).
 // 128 KiB LDS (2 buffers x {A 32 KiB, W 32 KiB}), one block per CU; one barrier per K-tile.
@@ -2133,17 +2010,6 @@ __global__ void to_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y
   if (i < n) y[i] = (bf16)x[i];
 }
 }  // namespace
-
-hipError_t patch_gemm_launch(const GemmParams& p, const float* img, int C, int HW, hipStream_t s) {
-  if (p.M <= 0) return hipSuccess;
-  if (HW % 16 || p.K != C * 256 || p.P != (HW / 16) * (HW / 16) || p.ntiles * GEMM_BN < p.N ||
-      (int64_t)p.M / p.P * C * HW * HW >= (1ll << 31))
-    return hipErrorInvalidValue;
-  const int mtiles = (p.M + GEMM_BM - 1) / GEMM_BM;
-  hipLaunchKernelGGL((patch_gemm_kernel<EPI_BIAS | EPI_POS | EPI_STATS>), dim3(mtiles * p.ntiles),
-                     dim3(256), 0, s, p, img, C, HW);
-  return hipGetLastError();
-}
 
 hipError_t to_bf16_launch(const float* x, void* y, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;

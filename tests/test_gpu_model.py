@@ -127,27 +127,3 @@ def test_graph_replay_matches_eager(gpu, dtype):
     torch.cuda.synchronize()
     assert torch.equal(logits, m(img))
 
-
-@pytest.mark.parametrize("batch", [1, 37])
-def test_fused_patch_gather_matches_patch_matrix_path(gpu, batch):
-    """The bf16 patch embedding with the gather in the GEMM's A loader (patch_gemm_kernel, default)
-    against the round-2 path (patchify_cm_kernel writes the bf16 patch matrix, then the GEMM;
-    selected by GEMM variant 9): both round the same pixels to bf16 and contract them in the same
-    K order, so the logits agree to the bf16 noise of the different tile shapes downstream."""
-    m = get_deit_tiny(dtype="bf16", seed=12, device=gpu, max_batch=batch)
-    img = torch.from_numpy(make_images(batch, seed=13)).to(gpu)
-    fused = m(img).clone()
-    lib = _lib_mod().load_library()
-    _lib_mod().check(lib.evt_set_gemm_variant(9))
-    try:
-        ref = m(img)
-    finally:
-        lib.evt_set_gemm_variant(0)
-    torch.cuda.synchronize()
-    err = float((fused - ref).abs().max())
-    assert err <= 2e-2, err
-
-
-def _lib_mod():
-    from edgevisiontransformer_amd import _lib
-    return _lib

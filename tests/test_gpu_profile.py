@@ -24,8 +24,7 @@ def test_profile_roles_deit_tiny(gpu, fusion):
     t0 = time.perf_counter()
     kt = kernel_times(m, img, logits, forwards=3)
     wall_us = (time.perf_counter() - t0) / 3 * 1e6  # per profiled forward (+ one extra)
-    # bf16: the patch gather runs inside the patch-embedding GEMM (no separate patchify launch)
-    expect = {"patch_embed": 1, "out_proj": 12, "fc1": 12, "fc2": 12, "head": 1}
+    expect = {"patchify": 1, "patch_embed": 1, "out_proj": 12, "fc1": 12, "fc2": 12, "head": 1}
     if fusion:
         expect["qkv_attention"] = 12
     else:
