@@ -203,19 +203,40 @@ __device__ __forceinline__ void load_frags(const T* rowp, bool valid, int lane, 
     f[c] = valid ? load4(rowp + 16 * c + 4 * (lane >> 4)) : f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
+// kptv^T-tile contraction over 16 tokens on MFMA: acc[j] += sum_t A[l&15][t] B[t][...] with A frags
+// (i = l & 15, k = t = 4(l>>4)+s) and B frags (k = t, j = l & 15) read as 4 consecutive tokens
+// from the per-wave transposed LDS tiles.
+template <typename T> __device__ __forceinline__ void tmma(f32x4& acc, const f32x4& a, const f32x4& b);
+template <> __device__ __forceinline__ void tmma<bf16>(f32x4& acc, const f32x4& a, const f32x4& b) {
+  const bf16x4 ah = {(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3]};
+  const bf16x4 bh = {(bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
+  acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(i16x4, ah),
+                                                  __builtin_bit_cast(i16x4, bh), acc, 0, 0, 0);
+}
+template <> __device__ __forceinline__ void tmma<float>(f32x4& acc, const f32x4& a, const f32x4& b) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
+}
+
 // grid (nchunk, B), block 256 (4 waves; wave w takes tiles w, w+4, ... of the chunk).
+// Per 16-token tile: kp = prm_exp(k) (MFMA chain), ksum partial (VALU), and
+// kptv[n][m] += sum_t v[t][n] kp[t][m] as 8 MFMAs (n tiles x m tiles, k = the 16 tokens): v and kp
+// are written transposed ([feature][token], fp32) to the wave's LDS so that each lane reads 4
+// consecutive tokens of one feature as its operand fragment.
 template <typename T>
 __global__ __launch_bounds__(256) void performer_kv_kernel(const T* __restrict__ kqv, int64_t ldq,
                                                            int ntok, int chunk,
                                                            const float* __restrict__ prmw,
                                                            float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) float smem[PF_M * 64 + 4 * 2 * 16 * 64 + 4 * PF_PART];
-  EVT_LDS float* wS = (EVT_LDS float*)smem;                    // [32][64] swz64
+  constexpr int TS = 20;  // floats per transposed row (16 tokens + 4 pad: conflict-light writes)
+  constexpr int TILES = 4 * (PF_HS + PF_M) * TS;
+  __shared__ __attribute__((aligned(16))) float smem[PF_M * 64 + (TILES > 4 * PF_PART ? TILES : 4 * PF_PART)];
+  EVT_LDS float* wS = (EVT_LDS float*)smem;                          // [32][64] swz64
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  EVT_LDS float* kpS = wS + PF_M * 64 + wave * 2 * 16 * 64;    // [16][64] swz64 (32 used)
-  EVT_LDS float* vS = kpS + 16 * 64;                           // [16][64] swz64
-  EVT_LDS float* red = wS + PF_M * 64 + 4 * 2 * 16 * 64;       // [4][PF_PART]
+  EVT_LDS float* vT = wS + PF_M * 64 + wave * (PF_HS + PF_M) * TS;  // [64 n][TS] (tokens)
+  EVT_LDS float* kT = vT + PF_HS * TS;                               // [32 m][TS]
+  EVT_LDS float* red = wS + PF_M * 64;  // [4][PF_PART], over the tiles once every wave is done
   const int b = blockIdx.y, ci = blockIdx.x;
   for (int i = tid; i < PF_M * PF_HS; i += 256) wS[swz64(i >> 6, i & 63)] = prmw[i];
   __syncthreads();
@@ -223,16 +244,19 @@ __global__ __launch_bounds__(256) void performer_kv_kernel(const T* __restrict__
   load_afrags<T>(wS, lane, fw);
   const int t_lo = ci * chunk, t_hi = min(ntok, t_lo + chunk);
   const float inv_sqrt_m = 1.0f / sqrtf((float)PF_M);
-  float acc[PF_M];  // kptv[n = lane][m]
+  f32x4 acc[4][2];  // kptv[n = 16 nt + 4 (l>>4) + j][m = 16 mt + (l & 15)]
 #pragma unroll
-  for (int m = 0; m < PF_M; ++m) acc[m] = 0.f;
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) acc[nt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float ks[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // ksum partial, m = 16mt + 4(l>>4) + j
+  const int tr = lane & 15, g4 = 4 * (lane >> 4);
   for (int t0 = t_lo + 16 * wave; t0 < t_hi; t0 += 64) {
-    const int t = t0 + (lane & 15);
+    const int t = t0 + tr;
     const bool valid = t < t_hi;
     const T* rowp = kqv + ((int64_t)b * ntok + t) * ldq;
     f32x4 kf[4], vf[4];
-    load_frags(rowp, valid, lane, kf);           // k = columns [0, 64)   (split order k, q, v)
+    load_frags(rowp, valid, lane, kf);              // k = columns [0, 64)   (split order k, q, v)
     load_frags(rowp + 2 * PF_HS, valid, lane, vf);  // v = columns [128, 192)
     float kd = 0.f;
 #pragma unroll
@@ -240,29 +264,28 @@ __global__ __launch_bounds__(256) void performer_kv_kernel(const T* __restrict__
     kd = 0.5f * token_sum(kd);
     f32x4 kp[2];
     prm_tile<T>(fw, kf, kd, inv_sqrt_m, kp);
-    const int tr = lane & 15;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       if (!valid) kp[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) ks[mt * 4 + j] += kp[mt][j];
-      *(EVT_LDS f32x4*)(kpS + swz64(tr, 16 * mt + 4 * (lane >> 4))) = kp[mt];
+      for (int j = 0; j < 4; ++j) {
+        ks[mt * 4 + j] += kp[mt][j];
+        kT[(16 * mt + g4 + j) * TS + tr] = kp[mt][j];
+      }
     }
 #pragma unroll
-    for (int c = 0; c < 4; ++c) *(EVT_LDS f32x4*)(vS + swz64(tr, 16 * c + 4 * (lane >> 4))) = vf[c];
-    __builtin_amdgcn_wave_barrier();
-    // kptv[n][m] += sum_t v[t][n] kp[t][m]   (lane = n)
-#pragma unroll 4
-    for (int tt = 0; tt < 16; ++tt) {
-      const float vn = vS[swz64(tt, lane)];
+    for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const f32x4 kq = *(const EVT_LDS f32x4*)(kpS + swz64(tt, 4 * q));
-        acc[4 * q + 0] += vn * kq[0];
-        acc[4 * q + 1] += vn * kq[1];
-        acc[4 * q + 2] += vn * kq[2];
-        acc[4 * q + 3] += vn * kq[3];
-      }
+      for (int j = 0; j < 4; ++j) vT[(16 * c + g4 + j) * TS + tr] = vf[c][j];
+    __builtin_amdgcn_wave_barrier();
+    f32x4 kb[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) kb[mt] = *(const EVT_LDS f32x4*)(kT + (16 * mt + tr) * TS + g4);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const f32x4 va = *(const EVT_LDS f32x4*)(vT + (16 * nt + tr) * TS + g4);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) tmma<T>(acc[nt][mt], va, kb[mt]);
     }
     __builtin_amdgcn_wave_barrier();
   }
@@ -272,9 +295,14 @@ __global__ __launch_bounds__(256) void performer_kv_kernel(const T* __restrict__
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) ks[i] += __shfl_xor(ks[i], o, 64);
   }
+  __syncthreads();  // every wave's tile loop is done: `red` reuses the tile area
   EVT_LDS float* myred = red + wave * PF_PART;
 #pragma unroll
-  for (int m = 0; m < PF_M; ++m) myred[lane * PF_M + m] = acc[m];
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) myred[(16 * nt + g4 + j) * PF_M + 16 * mt + tr] = acc[nt][mt][j];
   if ((lane & 15) == 0) {
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
@@ -551,6 +579,17 @@ hipError_t unfold_t(const void* in, int B, int H, int W, int C, int k, int s, in
 
 constexpr size_t PF_OUT_LDS = (size_t)(PF_M * 64 + 4 * 64 * 64 + 6 * 64) * sizeof(float);
 
+// fixed-order sum of an image's chunk partials: part[b][c][i] -> fin[b][i] (c ascending)
+__global__ __launch_bounds__(256) void performer_reduce_kernel(const float* __restrict__ part,
+                                                               int nchunk, float* __restrict__ fin) {
+  const int b = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= PF_PART) return;
+  const float* pb = part + (int64_t)b * nchunk * PF_PART + i;
+  float v = 0.f;
+  for (int c = 0; c < nchunk; ++c) v += pb[(int64_t)c * PF_PART];
+  fin[(int64_t)b * PF_PART + i] = v;
+}
+
 template <typename T>
 hipError_t performer_t(const void* kqv, int64_t ldq, int B, int ntok, int chunk, int nchunk,
                        float* part, const PerformerWeights& w, int span, void* out, int64_t ldo,
@@ -559,10 +598,14 @@ hipError_t performer_t(const void* kqv, int64_t ldq, int B, int ntok, int chunk,
                      ntok, chunk, w.prmw, part);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  // the chunk partials summed once per image (the output workgroups then read one partial each)
+  float* fin = part + (size_t)B * nchunk * PF_PART;
+  hipLaunchKernelGGL(performer_reduce_kernel, dim3((PF_PART + 255) / 256, B), dim3(256), 0, s,
+                     part, nchunk, fin);
   (void)hipFuncSetAttribute((const void*)performer_out_kernel<T>,
                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)PF_OUT_LDS);
   hipLaunchKernelGGL(performer_out_kernel<T>, dim3((ntok + span - 1) / span, B), dim3(256),
-                     PF_OUT_LDS, s, (const T*)kqv, ldq, ntok, span, part, nchunk, w, (T*)out, ldo);
+                     PF_OUT_LDS, s, (const T*)kqv, ldq, ntok, span, fin, 1, w, (T*)out, ldo);
   return hipGetLastError();
 }
 
@@ -580,10 +623,11 @@ hipError_t unfold_launch(int dtype, int in_f32, const void* in, int B, int H, in
   return unfold_t<float, float>(in, B, H, W, C, k, s, p, out, ldo, stats, nslots, st);
 }
 
-static int performer_chunks(int ntok) { return (ntok + 783) / 784; }
+// token chunks of the kv pass: >= 4 workgroups per image even at 28 x 28 tokens (stage 2)
+static int performer_chunks(int ntok) { return (ntok + 195) / 196; }
 
 size_t performer_part_floats(int B, int ntok) {
-  return (size_t)B * performer_chunks(ntok) * PF_PART;
+  return (size_t)B * (performer_chunks(ntok) + 1) * PF_PART;  // chunk partials + per-image sums
 }
 
 hipError_t performer_launch(int dtype, const void* kqv, int64_t ldq, int B, int ntok,
