@@ -439,6 +439,174 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void performer_out_ker
   }
 }
 
+// bf16 out pass with fewer registers and more waves: the weight fragments are read from LDS per
+// use (bf16 rows, 16-B chunks swizzled by row & 7; 34 KB per workgroup instead of 74 KB of fp32,
+// and ~128 fewer VGPRs than the register-resident fragments of performer_out_kernel), so three
+// workgroups share a CU, and the next tile's q / v rows are loaded while the current one runs.
+// Same arithmetic (bf16 operands, fp32 accumulation, same k order) as performer_out_kernel<bf16>.
+constexpr int PO_W = 0;                        // bf16 element offsets in the weight area:
+constexpr int PO_KV = PO_W + PF_M * 64;        // prm w [32][64], kptv [64][32],
+constexpr int PO_O = PO_KV + 64 * PF_M;        // out_w, fc1_w, fc2_w [64 out][64 in]
+constexpr int PO_1 = PO_O + 64 * 64;
+constexpr int PO_2 = PO_1 + 64 * 64;
+constexpr int PO_END = PO_2 + 64 * 64;
+constexpr size_t PF_OUT16_LDS = PO_END * 2 + 6 * 64 * sizeof(float);
+
+// element (r, c) of a bf16 matrix with `cols` columns (multiple of 8): row-major, 16-B chunk
+// (c / 8) stored at chunk index (c / 8) ^ (r & 7) (cols / 8 >= 4: chunk ^ (r & 3) when cols == 32)
+__device__ __forceinline__ int po_idx(int r, int c, int cols) {
+  const int nch = cols >> 3, q = (c >> 3) ^ (r & (nch - 1) & 7);
+  return r * cols + (q << 3) + (c & 7);
+}
+// A fragment (rows 16 rt + (l & 15), k columns 16 kc + 4 (l >> 4) .. + 3) as one 8-B LDS read
+__device__ __forceinline__ Afrag<bf16> po_frag(const EVT_LDS bf16* M, int cols, int rt, int kc, int lane) {
+  const int r = 16 * rt + (lane & 15), c = 16 * kc + 4 * (lane >> 4);
+  Afrag<bf16> f;
+  f.v = *(const EVT_LDS i16x4*)(M + po_idx(r, c, cols));
+  return f;
+}
+
+__global__ __launch_bounds__(256, 4) void performer_out16_kernel(const bf16* __restrict__ kqv,
+                                                                int64_t ldq, int ntok, int span,
+                                                                const float* __restrict__ part,
+                                                                PerformerWeights pw,
+                                                                bf16* __restrict__ out, int64_t ldo) {
+  extern __shared__ __attribute__((aligned(16))) char dsm16[];
+  EVT_LDS bf16* Wl = (EVT_LDS bf16*)dsm16;
+  EVT_LDS float* vec = (EVT_LDS float*)(dsm16 + PO_END * 2);  // ksum[64 (32 used)], bo, b1, b2, g2, be2
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.y;
+  for (int i = tid; i < PF_M * PF_HS; i += 256)  // prm w [m][k]
+    Wl[PO_W + po_idx(i >> 6, i & 63, 64)] = (bf16)pw.prmw[i];
+  for (int i = tid; i < 64 * 64; i += 256) {
+    const int kr = i >> 6, nc = i & 63;  // Keras [in = kr][out = nc] -> LDS [out][in]
+    Wl[PO_O + po_idx(nc, kr, 64)] = (bf16)pw.out_w[i];
+    Wl[PO_1 + po_idx(nc, kr, 64)] = (bf16)pw.fc1_w[i];
+    Wl[PO_2 + po_idx(nc, kr, 64)] = (bf16)pw.fc2_w[i];
+  }
+  const float* pb = part + (int64_t)b * PF_PART;  // the image's summed kptv / ksum
+  for (int i = tid; i < PF_PART; i += 256) {
+    const float v = pb[i];
+    if (i < PF_HS * PF_M) Wl[PO_KV + po_idx(i / PF_M, i % PF_M, PF_M)] = (bf16)v;
+    else vec[i - PF_HS * PF_M] = v;
+  }
+  for (int i = tid; i < 64; i += 256) {
+    vec[64 + i] = pw.out_b[i];
+    vec[128 + i] = pw.fc1_b[i];
+    vec[192 + i] = pw.fc2_b[i];
+    vec[256 + i] = pw.ln2_g[i];
+    vec[320 + i] = pw.ln2_b[i];
+  }
+  __syncthreads();
+  const float inv_sqrt_m = 1.0f / sqrtf((float)PF_M);
+  const int t_lo = blockIdx.x * span, t_hi = min(ntok, t_lo + span);
+  const int g4 = 4 * (lane >> 4);
+  // raw bf16 q / v of a tile: 4 + 4 pieces of 4 features (8 B each)
+  auto load_raw = [&](int t0, u32x2 (&r)[8]) {
+    const int t = t0 + (lane & 15);
+    const bool valid = t < t_hi;
+    const bf16* rowp = kqv + ((int64_t)b * ntok + (valid ? t : t_lo)) * ldq;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      r[c] = *(const u32x2*)(rowp + PF_HS + 16 * c + g4);
+      r[4 + c] = *(const u32x2*)(rowp + 2 * PF_HS + 16 * c + g4);
+    }
+  };
+  auto f4 = [](u32x2 v) {
+    const bf16x4 h = __builtin_bit_cast(bf16x4, v);
+    return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+  };
+  u32x2 raw[8];
+  int t0 = t_lo + 16 * wave;
+  if (t0 < t_hi) load_raw(t0, raw);
+  for (; t0 < t_hi; t0 += 64) {
+    const int t = t0 + (lane & 15);
+    const bool valid = t < t_hi;
+    // the weight fragments are re-read from LDS every tile, not hoisted into registers
+    const EVT_LDS bf16* Wt = Wl;
+    asm volatile("" : "+v"(Wt));
+    f32x4 qf[4], vf[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      qf[c] = valid ? f4(raw[c]) : f32x4{0.f, 0.f, 0.f, 0.f};
+      vf[c] = valid ? f4(raw[4 + c]) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (t0 + 64 < t_hi) load_raw(t0 + 64, raw);  // next tile in flight under this one
+    float qd = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) qd += qf[c][0] * qf[c][0] + qf[c][1] * qf[c][1] + qf[c][2] * qf[c][2] + qf[c][3] * qf[c][3];
+    qd = 0.5f * token_sum(qd);
+    f32x4 qp[2];  // prm_exp(q)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) chain16<bf16>(acc, po_frag(Wt + PO_W, 64, mt, c, lane), qf[c]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) qp[mt][j] = __expf(acc[j] - qd) * inv_sqrt_m;
+    }
+    float dn = 0.f;  // D_t = qp . ksum  (transformer_encoder.py:86)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dn += qp[mt][j] * vec[16 * mt + g4 + j];
+    const float rden = 1.0f / (token_sum(dn) + 1e-8f);
+    f32x4 y[4];  // y^T = kptv . qp^T / (D + eps)   (:88-90)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int mc = 0; mc < 2; ++mc) chain16<bf16>(acc, po_frag(Wt + PO_KV, PF_M, nt, mc, lane), qp[mc]);
+      y[nt] = acc * rden;
+    }
+    f32x4 y2[4];  // y2 = v + attn_output(y)   (:93)
+    float s1 = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) chain16<bf16>(acc, po_frag(Wt + PO_O, 64, nt, c, lane), y[c]);
+      const f32x4 bo = *(const EVT_LDS f32x4*)(vec + 64 + 16 * nt + g4);
+      y2[nt] = acc + bo + vf[nt];
+      s1 += y2[nt][0] + y2[nt][1] + y2[nt][2] + y2[nt][3];
+    }
+    const float mu = token_sum(s1) * (1.0f / 64.0f);
+    float s2 = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const f32x4 d = y2[nt] - mu;
+      s2 += d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3];
+    }
+    const float rstd = rsqrtf(token_sum(s2) * (1.0f / 64.0f) + 1e-5f);
+    f32x4 hn[4];  // LN2(y2)   (:99 norm2)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const f32x4 g = *(const EVT_LDS f32x4*)(vec + 256 + 16 * nt + g4);
+      const f32x4 be = *(const EVT_LDS f32x4*)(vec + 320 + 16 * nt + g4);
+      hn[nt] = (y2[nt] - mu) * rstd * g + be;
+    }
+    f32x4 h1[4];  // gelu(Dense(64))   (ffn.py:8)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) chain16<bf16>(acc, po_frag(Wt + PO_1, 64, nt, c, lane), hn[c]);
+      acc += *(const EVT_LDS f32x4*)(vec + 128 + 16 * nt + g4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) h1[nt][j] = gelu_tanh(acc[j]);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {  // out = y2 + Dense(64)(h1)   (ffn.py:9, :99)
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) chain16<bf16>(acc, po_frag(Wt + PO_2, 64, nt, c, lane), h1[c]);
+      acc += *(const EVT_LDS f32x4*)(vec + 192 + 16 * nt + g4) + y2[nt];
+      if (valid) store4(out + ((int64_t)b * ntok + t) * ldo + 16 * nt + g4, acc);
+    }
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(64) void cls_rows_kernel(T* __restrict__ x, int ntok, int D,
                                                       const float* __restrict__ cls,
@@ -602,6 +770,11 @@ hipError_t performer_t(const void* kqv, int64_t ldq, int B, int ntok, int chunk,
   float* fin = part + (size_t)B * nchunk * PF_PART;
   hipLaunchKernelGGL(performer_reduce_kernel, dim3((PF_PART + 255) / 256, B), dim3(256), 0, s,
                      part, nchunk, fin);
+  if constexpr (std::is_same<T, bf16>::value) {
+    hipLaunchKernelGGL(performer_out16_kernel, dim3((ntok + span - 1) / span, B), dim3(256),
+                       PF_OUT16_LDS, s, (const bf16*)kqv, ldq, ntok, span, fin, w, (bf16*)out, ldo);
+    return hipGetLastError();
+  }
   (void)hipFuncSetAttribute((const void*)performer_out_kernel<T>,
                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)PF_OUT_LDS);
   hipLaunchKernelGGL(performer_out_kernel<T>, dim3((ntok + span - 1) / span, B), dim3(256),
