@@ -572,11 +572,12 @@ __device__ __forceinline__ void big8_bar() {
   asm volatile("" ::: "memory");
 }
 
-// DMA region j of K-tile T into buffer T & 1.
+// DMA region j of K-tile T into buffer (T ^ par) & 1 (par: the buffer parity of the tile's
+// K-tile 0; persistent kernel with an odd K-tile count: alternates from tile to tile).
 __device__ __forceinline__ void big8_stage(const GemmParams& p, char* smem, int wave, int lane,
-                                           int m0, int n0, int T, int j) {
+                                           int m0, int n0, int T, int j, int par = 0) {
   const int srow = lane >> 3, sslot = lane & 7;
-  EVT_LDS char* base = (EVT_LDS char*)smem + (T & 1) * BIG_STAGE;
+  EVT_LDS char* base = (EVT_LDS char*)smem + ((T ^ par) & 1) * BIG_STAGE;
   const int64_t koff = (int64_t)T * ROWB + ((sslot ^ srow) << 4);
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -596,13 +597,13 @@ __device__ __forceinline__ void big8_stage(const GemmParams& p, char* smem, int 
 __device__ __forceinline__ int big8_npro(int nk) { return min(6, 4 * nk); }
 
 __device__ __forceinline__ void big8_prologue(const GemmParams& p, char* smem, int wave, int lane,
-                                              int m0, int n0, int nk) {
+                                              int m0, int n0, int nk, int par = 0) {
   // regions s = 0..5 (tile 0, then regions 0 / 1 of tile 1); only 0..3 when nk == 1
 #pragma unroll
-  for (int s = 0; s < 4; ++s) big8_stage(p, smem, wave, lane, m0, n0, 0, s);
+  for (int s = 0; s < 4; ++s) big8_stage(p, smem, wave, lane, m0, n0, 0, s, par);
   if (nk >= 2) {
-    big8_stage(p, smem, wave, lane, m0, n0, 1, 0);
-    big8_stage(p, smem, wave, lane, m0, n0, 1, 1);
+    big8_stage(p, smem, wave, lane, m0, n0, 1, 0, par);
+    big8_stage(p, smem, wave, lane, m0, n0, 1, 1, par);
   }
 }
 
@@ -620,9 +621,9 @@ template <int MODE, int X, bool OPEN = false, int X3 = 0, typename Ph3 = NoOp>
 __device__ __forceinline__ void big8_ktile(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
                                            int wave, int lane, int wm, int wn, int m0, int n0,
                                            int t, bool cont = false, int nm0 = 0, int nn0 = 0,
-                                           Ph3 ph3 = {}) {
+                                           Ph3 ph3 = {}, int par = 0, int npar = 0) {
   const int frow = lane & 15, fsw = lane & 7, fg = lane >> 4;
-  const EVT_LDS char* As = (const EVT_LDS char*)smem + (t & 1) * BIG_STAGE;
+  const EVT_LDS char* As = (const EVT_LDS char*)smem + ((t ^ par) & 1) * BIG_STAGE;
   const EVT_LDS char* Ws = As + BIG_TILE;
   auto rd = [&](const EVT_LDS char* S, int row, int ks) {
     return *(const EVT_LDS u32x4*)(S + row * ROWB + (((fg + 4 * ks) ^ fsw) << 4));
@@ -653,11 +654,11 @@ __device__ __forceinline__ void big8_ktile(const GemmParams& p, char* smem, f32x
     if (ph == 3) ph3();
     // DMA of region s = 4 t + ph + 6
     if (MODE == 0 || (MODE == 1 && ph < 2)) {
-      if (ph < 2) big8_stage(p, smem, wave, lane, m0, n0, t + 1, ph + 2);
-      else big8_stage(p, smem, wave, lane, m0, n0, t + 2, ph - 2);
+      if (ph < 2) big8_stage(p, smem, wave, lane, m0, n0, t + 1, ph + 2, par);
+      else big8_stage(p, smem, wave, lane, m0, n0, t + 2, ph - 2, par);
     } else if (cont) {  // MODE 1 phases 2, 3 and MODE 2: the next tile's regions, in order
       const int s6 = (MODE == 1 ? ph - 2 : ph + 2);  // 0..5: (K-tile 0, regions 0-3), (1, 0-1)
-      big8_stage(p, smem, wave, lane, nm0, nn0, s6 >> 2, s6 & 3);
+      big8_stage(p, smem, wave, lane, nm0, nn0, s6 >> 2, s6 & 3, npar);
     }
     // retire what the next phase reads (phases 4, 1, 2 precede reading phases)
     if (ph != 2) {
@@ -704,7 +705,10 @@ __device__ __forceinline__ void big8_loop(const GemmParams& p, char* smem, f32x4
                                           int wave, int lane, int wm, int wn, int m0, int n0,
                                           int nk, bool cont = false, int nm0 = 0, int nn0 = 0,
                                           Pre1 pre1 = {}, Mid mid = {}, Last last = {},
-                                          Last3 last3 = {}) {
+                                          Last3 last3 = {}, int par = 0) {
+  // K-tile t of this tile sits in buffer (t ^ par) & 1; the next tile (cont) starts at the parity
+  // of stream K-tile nk
+  const int npar = par ^ (nk & 1);
   if (nk >= 2) wait_vm<8 + X>();
   else wait_vm<4 + X>();
   big8_bar();
@@ -713,23 +717,24 @@ __device__ __forceinline__ void big8_loop(const GemmParams& p, char* smem, f32x4
     big8_bar();
   }
   if (nk >= 3) {
-    big8_ktile<0, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0);
+    big8_ktile<0, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, false, 0, 0, {}, par);
     mid();
     int t = 1;
-    for (; t + 2 < nk; ++t) big8_ktile<0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t);
-    big8_ktile<1, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, cont, nm0, nn0);
+    for (; t + 2 < nk; ++t)
+      big8_ktile<0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, false, 0, 0, {}, par);
+    big8_ktile<1, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, cont, nm0, nn0, {}, par, npar);
     last();
     big8_ktile<2, LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1, cont, nm0, nn0,
-                                 last3);
+                                 last3, par, npar);
   } else if (nk == 2) {
-    big8_ktile<1, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, cont, nm0, nn0);
+    big8_ktile<1, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, cont, nm0, nn0, {}, par, npar);
     last();
     big8_ktile<2, LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, 1, cont, nm0, nn0,
-                                 last3);
+                                 last3, par, npar);
   } else {
     last();
     big8_ktile<2, X + LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, false, 0, 0,
-                                     last3);
+                                     last3, par);
   }
   if (!OPEN && wm == 0) big8_bar();
 }
@@ -1203,7 +1208,7 @@ template <int FL, int DBG = 0, bool PADN = true, int ER = 0>
 __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
                                               int wave, int wm, int wn, int m0, int n0, int tn,
                                               int lane, bool interior, int iter = 0,
-                                              const u32x4 (*rre)[4] = nullptr) {
+                                              const u32x4 (*rre)[4] = nullptr, int spar = 0) {
   // DBG 3: sub-stamps 3..5 of the tile's timeline row (wave 0, lane 0)
   auto stamp = [&](int k) {
     if (DBG == 3 && wave == 0 && lane == 0 && iter < 16)
@@ -1380,7 +1385,9 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
   //    phases 1 / 2) and leaves as whole 128-B row segments, 8 rows per store instruction
   {
     const int w = wave;
-    EVT_LDS char* scr = (EVT_LDS char*)smem +
+    // spar: buffer parity of the next tile, whose K-tile 1 (regions 2 / 3 still unloaded) sits in
+    // buffer 1 ^ spar
+    EVT_LDS char* scr = (EVT_LDS char*)smem - spar * BIG_STAGE +
                         (w < 4 ? (96 + 4 + 8 * w) * 1024 : (72 + (w - 4) * 4 + ((w - 4) >> 1) * 8) * 1024);
     const int wrow = (fg & 1) * 16 + frow;               // store-layout row within the pair
     const int rrow = lane >> 3, rch = lane & 7;          // row-layout lane: row i*8 + rrow, chunk
@@ -1473,6 +1480,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
   pers_coop_dma<FL>(p, smem, wave, lane, tm * BIG_BM, tn * BIG_BN);
   big8_prologue(p, smem, wave, lane, tm * BIG_BM, tn * BIG_BN, nk);
   wait_vmcnt0();  // the first K-tile's waits assume PERS_X younger VMEM ops or a drain
+  int par = 0;    // buffer parity of this tile's K-tile 0 (the stream alternates it for odd nk)
   // nk >= 3: per-tile LayerNorm coefficients / next statistics DMA inside the main loop
   const bool early = nk >= 3 && DBG != 16 && DBG != 17;
   int iter = 0;
@@ -1498,8 +1506,10 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
       ntm = next / p.ntiles;
       ntn = next - ntm * p.ntiles;
     }
-    // even nk: the next tile's prologue rides in the last K-tiles' idle DMA slots (big8_ktile)
-    const bool cont = has_next && !(nk & 1) && DBG != 16;
+    // the next tile's prologue rides in the last K-tiles' idle DMA slots (big8_ktile) as K-tiles
+    // nk, nk + 1 of one stream: for odd nk the next tile starts at the other buffer parity
+    const bool cont = has_next && nk >= 2 && DBG != 16 && (DBG != 6 || !(nk & 1));
+    const int npar = cont ? par ^ (nk & 1) : 0;
     auto last = [&]() {
       if constexpr (ER > 0) pers_resid_early<0, 1>(p, wm, wn, ln, m0, n0, rre);
     };
@@ -1516,18 +1526,18 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
       };
       if constexpr (DBG == 18)  // A/B: groups re-synchronised before the epilogue
         big8_loop<PERS_X>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
-                          ntn * BIG_BN, pre1, mid);
+                          ntn * BIG_BN, pre1, mid, {}, {}, par);
       else
         big8_loop<PERS_X, true, decltype(pre1), decltype(mid), (ER > 0 ? 4 : 0), decltype(last),
                   (ER > 1 ? 4 : 0), decltype(last3)>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont,
                                                    ntm * BIG_BM, ntn * BIG_BN, pre1, mid, last,
-                                                   last3);
+                                                   last3, par);
       stamp(1);
       if (has_next && !cont) big8_prologue(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nk);
     } else {
       big8_loop<PERS_X, false, NoOp, NoOp, (ER > 0 ? 4 : 0), decltype(last), (ER > 1 ? 4 : 0),
                 decltype(last3)>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
-                                 ntn * BIG_BN, {}, {}, last, last3);
+                                 ntn * BIG_BN, {}, {}, last, last3, par);
       stamp(1);
       pers_coef<FL>(p, smem, tid);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1545,11 +1555,12 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
       pers_epilogue_v1<FL, 0, PADN>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior);
     else
       pers_epilogue<FL, DBG, PADN, ER>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior, iter,
-                                       rre);
+                                       rre, npar);
     stamp(7);
     ++iter;
     if (!has_next) break;
     if (!interior || DBG == 1 || DBG == 2) wait_vmcnt0();
+    par = npar;
     tile = next;
     tm = ntm;
     tn = ntn;

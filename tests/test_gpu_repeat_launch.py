@@ -139,3 +139,25 @@ def test_repeat_attention(gpu):
     p = torch.softmax(torch.einsum("bhid,bhjd->bhij", q, k) * 0.125, dim=-1)
     ref = torch.einsum("bhij,bhjd->bhid", p, v).permute(0, 2, 1, 3).reshape(M, D)
     torch.testing.assert_close(got.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("M,K,N", [(50176, 192, 576), (50176, 576, 192), (50176, 192, 192)])
+def test_repeat_odd_ktile_count(gpu, M, K, N):
+    """Persistent GEMM with an odd number of 64-wide K-tiles (Swin stage-2 QKV K = 192, T2T kqv
+    K = 576): the next tile's prologue rides in the current tile's last K-tiles at the other LDS
+    buffer parity, and the epilogue's scratch moves with it. Every launch bitwise equal to the
+    first, the first against an fp32 reference (LN-folded input, as the Swin / T2T QKV)."""
+    x = (_randn((M, K), 160 + K, 1.2) + 0.1).bfloat16()
+    g, be = 1.0 + _randn((K,), 161, 0.1), _randn((K,), 162, 0.1)
+    W, bias = _randn((K, N), 163, 1 / math.sqrt(K)), _randn((N,), 164, 0.05)
+    wp, kpad, npad = _ops.pack(W, "bf16", row_scale=g)
+    colsum, cvec = _ops.ln_fold("bf16", wp, kpad, npad, W, be, bias)
+    st = _stats(x)
+    C = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+
+    def launch():
+        _ops.dense("bf16", _lib.EPI_LNIN | _lib.EPI_BIAS, x, wp, kpad, npad, M, N, bias=cvec,
+                   colsum=colsum, stats_in=st, ln_width=K, C=C)
+    (got,) = _repeat(launch, [C])
+    ref = _ln(x.float(), g, be) @ W + bias
+    torch.testing.assert_close(got.float(), ref, rtol=2.5e-2, atol=2.5e-2)
