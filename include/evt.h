@@ -315,7 +315,8 @@ int evt_performer(int dtype, const void* kqv, int64_t ldq, int B, int T, const f
                   const float* fc1_w, const float* fc1_b, const float* fc2_w, const float* fc2_b,
                   float* part, void* out, int64_t ldo, void* stream);
 
-/* fp32 scratch elements evt_performer needs for B images of T tokens. */
+/* fp32 scratch elements evt_performer needs for B images of T tokens: per image, a (kptv, ksum)
+ * partial of 64*32 + 32 floats per 196-token chunk and their sum. */
 int64_t evt_performer_scratch(int B, int T);
 
 /* ---- Swin Transformer (reference utils.py:14-47 get_swin -> microsoft SwinTransformer) ---- */

@@ -97,7 +97,9 @@ def test_t2t_host_validation(lib):
     assert lib.evt_t2t_create(ctypes.byref(d), None, 0, None, ctypes.byref(h)) == _lib.EVT_EINVAL
     assert lib.evt_unfold(1, 1, None, 1, 8, 8, 3, 7, 4, 2, None, 147, None, 0, None) == _lib.EVT_EINVAL
     assert lib.evt_performer(1, None, 192, 1, 16, *([None] * 10), None, 64, None) == _lib.EVT_EINVAL
-    assert lib.evt_performer_scratch(2, 3136) == 2 * 4 * (64 * 32 + 32)
+    # per image: one (kptv, ksum) partial per 196-token chunk + their sum (t2t.hip performer_t)
+    assert lib.evt_performer_scratch(2, 3136) == 2 * (16 + 1) * (64 * 32 + 32)
+    assert lib.evt_performer_scratch(3, 784) == 3 * (4 + 1) * (64 * 32 + 32)
 
 
 def test_swin_host_validation(lib):
