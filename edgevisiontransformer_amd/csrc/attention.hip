@@ -275,8 +275,12 @@ __global__ __launch_bounds__(256, (NKT == 13 || NKT == 12) ? 3 : 1) void attn_bf
   }
 }
 
+#ifndef ATTN_F32_WAVES
+#define ATTN_F32_WAVES 8
+#endif
+
 template <int NKT>
-__global__ __launch_bounds__(256) void attn_f32_kernel(AttnParams p) {
+__global__ __launch_bounds__(64 * ATTN_F32_WAVES) void attn_f32_kernel(AttnParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NP = NKT * 16;
   constexpr int ROWB = 256;  // 64 fp32
@@ -289,7 +293,7 @@ __global__ __launch_bounds__(256) void attn_f32_kernel(AttnParams p) {
 
   {
     const int srow = lane >> 4, sslot = lane & 15;  // 4 rows of 256 B per wave-instruction
-    for (int i = wave; i < NP / 4; i += 4) {
+    for (int i = wave; i < NP / 4; i += ATTN_F32_WAVES) {
       const int row = i * 4 + srow;
       const int gr = min(row, p.N - 1);
       const float* rp = qkv + (int64_t)gr * p.ldq + ((sslot ^ (row & 15)) * 4);
@@ -302,7 +306,7 @@ __global__ __launch_bounds__(256) void attn_f32_kernel(AttnParams p) {
 
   const int g = lane >> 4, c16 = lane & 15;
   const int nqt = (p.N + 15) >> 4;
-  for (int qt = wave; qt < nqt; qt += 4) {
+  for (int qt = wave; qt < nqt; qt += ATTN_F32_WAVES) {
     const int qi = min(qt * 16 + c16, p.N - 1);
     const float* qrow = qkv + (int64_t)qi * p.ldq + h * 64;
     f32x4 qf[4];
@@ -357,20 +361,21 @@ __global__ __launch_bounds__(256) void attn_f32_kernel(AttnParams p) {
       for (int e = 0; e < 4; ++e) {
         __builtin_amdgcn_sched_barrier(0);
         const int key = kt * 16 + 4 * g + e;
-        const EVT_LDS char* vr = Vs + key * ROWB;
+        // MFMA row m of o[dt] is head dim d = 4 m + dt: the lane's four V values are one 16-byte
+        // LDS chunk (d = 4 c16 .. 4 c16 + 3)
+        const f32x4 v = *(const EVT_LDS f32x4*)(Vs + key * ROWB + ((c16 ^ (key & 15)) * 16));
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          const int d = dt * 16 + c16;
-          const float v = *(const EVT_LDS float*)(vr + (((d >> 2) ^ (key & 15)) * 16) + (d & 3) * 4);
-          o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, s[kt][e], o[dt], 0, 0, 0);
-        }
+        for (int dt = 0; dt < 4; ++dt)
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[dt], s[kt][e], o[dt], 0, 0, 0);
       }
     const int q = qt * 16 + c16;
     if (q < p.N) {
       const float inv = 1.0f / sum;
-      float* op = (float*)p.out + ((int64_t)b * p.N + q) * p.ldo + h * 64 + 4 * g;
+      // lane holds O[d = 16 g + 4 j + dt][q] in o[dt][j]
+      float* op = (float*)p.out + ((int64_t)b * p.N + q) * p.ldo + h * 64 + 16 * g;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) store4(op + dt * 16, o[dt] * inv);
+      for (int j = 0; j < 4; ++j)
+        store4(op + 4 * j, f32x4{o[0][j], o[1][j], o[2][j], o[3][j]} * inv);
     }
   }
 }
@@ -385,7 +390,7 @@ hipError_t launch_nkt(int dtype, const AttnParams& p, hipStream_t s) {
   if (dtype == DT_BF16)
     hipLaunchKernelGGL((attn_bf16_kernel<NKT, 5>), dim3(p.B * p.H), dim3(256), lds, s, p);
   else if constexpr (NKT % 2 == 0)
-    hipLaunchKernelGGL(attn_f32_kernel<NKT>, dim3(p.B * p.H), dim3(256), lds, s, p);
+    hipLaunchKernelGGL(attn_f32_kernel<NKT>, dim3(p.B * p.H), dim3(64 * ATTN_F32_WAVES), lds, s, p);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
