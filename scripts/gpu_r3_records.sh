@@ -7,7 +7,7 @@ O=gpurun_out/${TAG:-r3rec}
 mkdir -p $O
 export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-summ() { python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().split('\n')[-1]); r=d['roofline'] or {}; print(d['config']['model'], d['value'], d['ms_per_step'], 'model', d['model_roofline']['frac'], 'dom', r.get('role'), r.get('frac'), 'hbm', r.get('hbm_frac'), 'cpu', (d['cpu_baseline'] or {}).get('value')); [print('  ', k, v) for k, v in (r.get('per_role') or {}).items()]" $1; }
+summ() { python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); r=d['roofline'] or {}; print(d['config']['model'], d['value'], d['ms_per_step'], 'model', d['model_roofline']['frac'], 'dom', r.get('role'), r.get('frac'), 'hbm', r.get('hbm_frac'), 'cpu', (d['cpu_baseline'] or {}).get('value')); [print('  ', k, v) for k, v in (r.get('per_role') or {}).items()]" $1; }
 if [ -z "${SKIP_TESTS:-}" ]; then
   timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests -m gpu > $O/pytest_gpu.log 2>&1
   rc=$?; tail -2 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
