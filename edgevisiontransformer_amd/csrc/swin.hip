@@ -473,8 +473,11 @@ __global__ __launch_bounds__(256) void ln_pool_kernel(const T* __restrict__ x, i
 constexpr int MLP96_C = 96, MLP96_F = 384;
 constexpr int MLP96_W1_ROW = 208, MLP96_W2_ROW = 784;
 constexpr int MLP96_LDS = MLP96_F * MLP96_W1_ROW + MLP96_C * MLP96_W2_ROW;  // 155136 B
+// 12 waves (3 per SIMD, <= 168 VGPRs): the MFMA -> GELU -> MFMA chain of one wave leaves the
+// SIMD idle on latencies that a third wave fills
+constexpr int MLP96_WAVES = 12;
 
-__global__ __launch_bounds__(512, 1) void swin_mlp96_kernel(SwinMlpParams p) {
+__global__ __launch_bounds__(64 * MLP96_WAVES, 1) void swin_mlp96_kernel(SwinMlpParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   EVT_LDS char* W1s = (EVT_LDS char*)smem;
   EVT_LDS char* W2s = W1s + MLP96_F * MLP96_W1_ROW;
@@ -483,11 +486,11 @@ __global__ __launch_bounds__(512, 1) void swin_mlp96_kernel(SwinMlpParams p) {
   const bf16* w1 = (const bf16*)p.w1;
   const bf16* w2 = (const bf16*)p.w2;
   // ---- stage the weights (once per block) ----
-  for (int e = tid; e < MLP96_F * 12; e += 512) {  // W1: row n, 16-B chunk j of 12
+  for (int e = tid; e < MLP96_F * 12; e += 64 * MLP96_WAVES) {  // W1: row n, 16-B chunk j of 12
     const int n = e / 12, j = e - n * 12;
     *(EVT_LDS u32x4*)(W1s + n * MLP96_W1_ROW + j * 16) = *(const u32x4*)(w1 + (int64_t)n * p.ldw1 + j * 8);
   }
-  for (int e = tid; e < MLP96_C * 48; e += 512) {  // W2: row c, chunk (hc, gg) of 12 x 4
+  for (int e = tid; e < MLP96_C * 48; e += 64 * MLP96_WAVES) {  // W2: row c, chunk (hc, gg) of 12 x 4
     const int c = e / 48, r = e - c * 48, hc = r >> 2, gg = r & 3;
     const bf16* src = w2 + (int64_t)c * p.ldw2 + hc * 32 + 4 * gg;
     const uint2 lo = *(const uint2*)src;         // hidden 32 hc + 4 gg .. + 3
@@ -497,7 +500,7 @@ __global__ __launch_bounds__(512, 1) void swin_mlp96_kernel(SwinMlpParams p) {
   __syncthreads();
   const float inv_d = 1.0f / (float)MLP96_C;
   const int ntiles = (p.M + 31) / 32;
-  for (int t = blockIdx.x * 8 + wave; t < ntiles; t += gridDim.x * 8) {
+  for (int t = blockIdx.x * MLP96_WAVES + wave; t < ntiles; t += gridDim.x * MLP96_WAVES) {
     const int tok0 = t * 32;
     // B operand of FC1: LN2(xm) of token (16 tt + c16), k 32 ks + 8 g .. + 7, normalised in
     // registers ((x - mu) r; gamma is folded into W1, beta.W1 + b1 = cvec seeds the accumulator)
@@ -606,58 +609,72 @@ __global__ __launch_bounds__(512, 1) void swin_mlp96_kernel(SwinMlpParams p) {
 
 // ---- fused attention sublayer of the C = 96 stage (Swin-T / Swin-S stage 1) --------------------
 // xm = x + proj(WMSA(LN1(x))) for one 7x7 window per block iteration, everything between the x
-// read and the xm write in LDS: the separate QKV GEMM, window attention and proj move 1.7 GB per
+// read and the xm write on chip: the separate QKV GEMM, window attention and proj move 1.7 GB per
 // stage-1 block (qkv 462 MB written + read, o 154 MB written + read, x / xm); here 0.3 GB.
-//   LDS: Wq (QKV, 288 rows x 96 k, LN1 gamma folded) and Wp (proj, 96 x 96), loaded once per
-//   block; per window Xn = LN1(x) of the 49 (64) window tokens (gathered with the cyclic shift),
-//   the window's qkv [64][288] and o [64][96] (bf16).
-//   Phases (8 waves, barriers between): Xn staging; QKV = Wq . Xn^T (+ beta.W + b seeds the
-//   accumulators); 12 (head, query tile) attention units exactly as window_attn_bf16_kernel but
-//   with Q / K / V from LDS; proj = Wp . O^T + b + x (raw rows) -> xm, row statistics.
-constexpr int AT96_ROW = 208;                      // 96-element rows (+ 8 pad)
-constexpr int AT96_QROW = 592;                     // 288-element qkv rows (+ 8 pad)
-constexpr int AT96_WQ = 0;
-constexpr int AT96_WP = AT96_WQ + 288 * AT96_ROW;  // 59904
-constexpr int AT96_XN = AT96_WP + 96 * AT96_ROW;   // 79872
-constexpr int AT96_QKV = AT96_XN + 64 * AT96_ROW;  // 93184
-constexpr int AT96_O = AT96_QKV + 64 * AT96_QROW;  // 131072
-constexpr int AT96_XR = AT96_O + 64 * AT96_ROW;    // 144384: raw x rows (the residual)
-constexpr int AT96_PART = AT96_XR + 64 * AT96_ROW; // 157696
-constexpr int AT96_LDS = AT96_PART + 2 * 64 * 8;   // 158720
+// The per-window work is small and latency-bound (three short phases separated by barriers), so
+// the kernel is sized for TWO blocks per CU, whose phases interleave: 4 waves and 71 KiB of LDS
+// per block. The QKV weights (288 x 96, LN1 gamma folded) live in registers, split by feature
+// tile over the waves (5 / 5 / 4 / 4 of 18 tiles: 60 VGPRs); LDS holds the proj weights (96 x 96),
+// the window's qkv [64][288] and one [64][96] buffer that is Xn = LN1(x) of the 49 (64) window
+// tokens (gathered with the cyclic shift) in P1, the attention output O in P2 / P3 and the xm
+// staging rows at the end.
+//   P0  Xn ((x - mu) r, rows past 49 zero) from the x chunks prefetched during the previous
+//       window's attention                                                       -> barrier
+//   P1  QKV^T = Wq . Xn^T (+ beta.W + b seeds), wave = its feature tiles x all 4 token tiles
+//                                                                                -> barrier
+//   P2  attention units (head h, query tile `wave`) for h = 0..2, exactly as window_attn_bf16 with
+//       Q / K / V from LDS; O rows 16 wave .. 16 wave + 15 are written by this wave only, so
+//   P3  (no barrier) proj = Wp . O^T + b + x (rows re-read from L2) -> bf16 xm, full-row
+//       statistics in the wave (lane groups hold the 4 column quarters), xm staged through the
+//       wave's own O rows and stored as whole 192-B rows (16-B pieces).
+constexpr int AT96_ROW = 208;                       // 96-element rows (+ 8 pad)
+constexpr int AT96_QROW = 592;                      // 288-element qkv rows (+ 8 pad)
+constexpr int AT96_WP = 0;                          // proj weights [96][AT96_ROW]
+constexpr int AT96_QKV = AT96_WP + 96 * AT96_ROW;   // 19968: window qkv [64][AT96_QROW]
+constexpr int AT96_XO = AT96_QKV + 64 * AT96_QROW;  // 57856: Xn / O / xm staging [64][AT96_ROW]
+constexpr int AT96_CV = AT96_XO + 64 * AT96_ROW;    // 71168: cqkv [288], bproj [96] (f32)
+constexpr int AT96_LDS = AT96_CV + 384 * 4;         // 72704: two blocks per CU
 
-__global__ __launch_bounds__(512, 1) void swin_attn96_kernel(SwinAttnBlockParams p) {
+__global__ __launch_bounds__(256, 2) void swin_attn96_kernel(SwinAttnBlockParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   EVT_LDS char* L = (EVT_LDS char*)smem;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, c16 = lane & 15;
   const bf16* x = (const bf16*)p.x;
-  // ---- weights, once per block ----
-  for (int e = tid; e < 288 * 12; e += 512) {
-    const int n = e / 12, j = e - n * 12;
-    *(EVT_LDS u32x4*)(L + AT96_WQ + n * AT96_ROW + j * 16) =
-        *(const u32x4*)((const bf16*)p.wqkv + (int64_t)n * p.ldq + j * 8);
-  }
-  for (int e = tid; e < 96 * 12; e += 512) {
+  // ---- once per block: Wp / cqkv / bproj -> LDS, this wave's Wq fragments -> registers ----
+  for (int e = tid; e < 96 * 12; e += 256) {
     const int n = e / 12, j = e - n * 12;
     *(EVT_LDS u32x4*)(L + AT96_WP + n * AT96_ROW + j * 16) =
         *(const u32x4*)((const bf16*)p.wproj + (int64_t)n * p.ldp + j * 8);
   }
-  const int nwx = p.R / 7, nw = nwx * nwx;
+  for (int e = tid; e < 384; e += 256)
+    ((EVT_LDS float*)(L + AT96_CV))[e] = e < 288 ? p.cqkv[e] : p.bproj[e - 288];
+  const int ft0 = wave * 5 - (wave > 2 ? 1 : 0), nft = wave < 2 ? 5 : 4;  // 0 / 5 / 10 / 14
+  u32x4 wq[5][3];
+#pragma unroll
+  for (int f = 0; f < 5; ++f)
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+      const int ft = min(ft0 + f, 17);
+      wq[f][ks] = *(const u32x4*)((const bf16*)p.wqkv + (int64_t)(16 * ft + c16) * p.ldq + 32 * ks + 8 * g);
+    }
+  const int nwx = p.R / 7, nw = nwx * nwx, nwin = p.B * nw;
   const float inv_d = 1.0f / 96.0f;
   const float scale_log2 = 0.17677669529663687f * kLog2e;
-  // x chunks (token e / 12, 16-B chunk e % 12; e = tid, tid + 512 < 768) and their row
-  // statistics of the NEXT window are loaded during the current window's attention phase
-  u32x4 xc[2];
-  f32x4 sc[2];
+  // x chunks (token e / 12, 16-B chunk e % 12; e = tid + 256 k) and their row statistics of the
+  // NEXT window, loaded during the current window's attention phase
+  u32x4 xc[3];
+  f32x4 sc[3];
   auto prefetch = [&](int wgn) {
     const int bn = wgn / nw, wn = wgn - bn * nw;
     const WinGeom Gn(p.R, nwx, p.shift, bn, wn);
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int e = tid + 512 * k, t = e / 12, j = e - t * 12;
+    for (int k = 0; k < 3; ++k) {
+      const int e = tid + 256 * k, t = e / 12, j = e - t * 12;
       xc[k] = u32x4{0u, 0u, 0u, 0u};
       sc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (e < 768 && t < 49) {
+      if (t < 49) {
         const int64_t row = Gn.row(t);
         xc[k] = *(const u32x4*)(x + row * 96 + j * 8);
         const float* st = p.stats_in + row * 2 * p.nslots;
@@ -665,19 +682,16 @@ __global__ __launch_bounds__(512, 1) void swin_attn96_kernel(SwinAttnBlockParams
       }
     }
   };
-  if (blockIdx.x < p.B * nw) prefetch(blockIdx.x);
-  f32x4 bpr[3];  // proj bias of this wave's feature tiles (P3), loaded once
-#pragma unroll
-  for (int f = 0; f < 3; ++f) bpr[f] = load4(p.bproj + 16 * ((wave >> 2) * 3 + f) + 4 * g);
-  for (int wg = blockIdx.x; wg < p.B * nw; wg += gridDim.x) {
+  if (blockIdx.x < nwin) prefetch(blockIdx.x);
+  const int tq = (lane >> 2) & 3, tp = lane & 3;
+  for (int wg = blockIdx.x; wg < nwin; wg += gridDim.x) {
     const int b = wg / nw, win = wg - b * nw;
     const WinGeom G(p.R, nwx, p.shift, b, win);
-    __syncthreads();  // previous window's readers of Xn / XR / QKV / O / part are done
-    // ---- P0: Xn = LN1(x) of the window tokens ((x - mu) r), XR = x (zero rows past 49) ----
+    __syncthreads();  // the previous window's qkv / XO readers are done
+    // ---- P0: Xn = LN1(x) of the window tokens ((x - mu) r; gamma is in Wq, beta in cqkv) ----
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int e = tid + 512 * k, t = e / 12, j = e - t * 12;
-      if (e >= 768) break;
+    for (int k = 0; k < 3; ++k) {
+      const int e = tid + 256 * k, t = e / 12, j = e - t * 12;
       u32x4 nv = u32x4{0u, 0u, 0u, 0u};
       if (t < 49) {  // (nslots <= 2 here: C = 96)
         const float s1 = sc[k][0] + sc[k][2], s2 = sc[k][1] + sc[k][3];
@@ -691,60 +705,58 @@ __global__ __launch_bounds__(512, 1) void swin_attn96_kernel(SwinAttnBlockParams
           nv[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(f, bf16x2));
         }
       }
-      *(EVT_LDS u32x4*)(L + AT96_XN + t * AT96_ROW + j * 16) = nv;
-      *(EVT_LDS u32x4*)(L + AT96_XR + t * AT96_ROW + j * 16) = xc[k];
+      *(EVT_LDS u32x4*)(L + AT96_XO + t * AT96_ROW + j * 16) = nv;
     }
     __syncthreads();
-    // ---- P1: QKV^T = Wq . Xn^T + cqkv; wave = token tile (wave & 3) x 9 feature tiles ----
+    // ---- P1: QKV^T = Wq . Xn^T + cqkv: this wave's feature tiles x the 4 token tiles ----
     {
-      const int tt = wave & 3, ft0 = (wave >> 2) * 9;
-      u32x4 bx[3];
+      u32x4 bx[4][3];
 #pragma unroll
-      for (int ks = 0; ks < 3; ++ks)
-        bx[ks] = *(const EVT_LDS u32x4*)(L + AT96_XN + (16 * tt + c16) * AT96_ROW + 64 * ks + 16 * g);
-#pragma unroll 3
-      for (int f = 0; f < 9; ++f) {
+      for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks)
+          bx[tt][ks] = *(const EVT_LDS u32x4*)(L + AT96_XO + (16 * tt + c16) * AT96_ROW + 64 * ks + 16 * g);
+#pragma unroll
+      for (int f = 0; f < 5; ++f) {
+        if (f >= nft) break;
         const int ft = ft0 + f;
-        f32x4 acc = load4(p.cqkv + 16 * ft + 4 * g);
+        const f32x4 cq = *(const EVT_LDS f32x4*)(L + AT96_CV + (16 * ft + 4 * g) * 4);
+        f32x4 acc[4] = {cq, cq, cq, cq};
 #pragma unroll
-        for (int ks = 0; ks < 3; ++ks) {
-          const u32x4 wv = *(const EVT_LDS u32x4*)(L + AT96_WQ + (16 * ft + c16) * AT96_ROW + 64 * ks + 16 * g);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wv),
-                                                        __builtin_bit_cast(bf16x8, bx[ks]), acc, 0, 0, 0);
+        for (int ks = 0; ks < 3; ++ks)
+#pragma unroll
+          for (int tt = 0; tt < 4; ++tt)
+            acc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wq[f][ks]),
+                                                              __builtin_bit_cast(bf16x8, bx[tt][ks]),
+                                                              acc[tt], 0, 0, 0);
+        // acc[tt][jj]: feature 16 ft + 4 g + jj, token 16 tt + c16
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+          const f32x2 lo = {acc[tt][0], acc[tt][1]}, hi = {acc[tt][2], acc[tt][3]};
+          const u32x2 pk = {__builtin_bit_cast(unsigned, __builtin_convertvector(lo, bf16x2)),
+                            __builtin_bit_cast(unsigned, __builtin_convertvector(hi, bf16x2))};
+          *(EVT_LDS u32x2*)(L + AT96_QKV + (16 * tt + c16) * AT96_QROW + (16 * ft + 4 * g) * 2) = pk;
         }
-        // acc[jj]: feature 16 ft + 4 g + jj, token 16 tt + c16
-        const f32x2 lo = {acc[0], acc[1]}, hi = {acc[2], acc[3]};
-        u32x2 pk = {__builtin_bit_cast(unsigned, __builtin_convertvector(lo, bf16x2)),
-                    __builtin_bit_cast(unsigned, __builtin_convertvector(hi, bf16x2))};
-        *(EVT_LDS u32x2*)(L + AT96_QKV + (16 * tt + c16) * AT96_QROW + (16 * ft + 4 * g) * 2) = pk;
       }
     }
     __syncthreads();
-    // ---- P2: attention, 12 (head, query tile) units over 8 waves (units wave, wave + 8) ----
-    // bias rows of both units first, then the next window's x prefetch: the in-order vmcnt
+    // ---- P2: attention units (h, query tile `wave`), h = 0..2 ----
+    // bias rows of the three units first, then the next window's x prefetch: the in-order vmcnt
     // makes every wait on a load also wait on the loads issued before it
-    f32x4 bvu[2][4];
+    const int qt = wave;
+    f32x4 bvu[3][4];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int u = wave + 8 * k;
-      if (u < 12) {
-        const int h = u >> 2, qt = u & 3;
-        const float* br = p.bias + ((int64_t)G.type() * 3 + h) * 49 * 64 +
-                          (int64_t)min(16 * qt + c16, 48) * 64 + 4 * g;
+    for (int h = 0; h < 3; ++h) {
+      const float* br = p.bias + ((int64_t)G.type() * 3 + h) * 49 * 64 +
+                        (int64_t)min(16 * qt + c16, 48) * 64 + 4 * g;
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt) bvu[k][kt] = *(const f32x4*)(br + 16 * kt);
-      }
+      for (int kt = 0; kt < 4; ++kt) bvu[h][kt] = *(const f32x4*)(br + 16 * kt);
     }
-    if (wg + (int)gridDim.x < p.B * nw) prefetch(wg + gridDim.x);  // lands during P2 / P3
-    const int tq = (lane >> 2) & 3, tp = lane & 3;
+    if (wg + (int)gridDim.x < nwin) prefetch(wg + gridDim.x);  // lands during P2 / P3
+    const EVT_LDS char* Q = L + AT96_QKV;
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int u = wave + 8 * k;
-      if (u >= 12) break;
-      const int h = u >> 2, qt = u & 3;
-      const EVT_LDS char* Q = L + AT96_QKV;
+    for (int h = 0; h < 3; ++h) {
       const u32x4 qf = *(const EVT_LDS u32x4*)(Q + (16 * qt + c16) * AT96_QROW + (32 * h + 8 * g) * 2);
-      const f32x4* bv = bvu[k];
       f32x4 sv[4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
@@ -756,8 +768,8 @@ __global__ __launch_bounds__(512, 1) void swin_attn96_kernel(SwinAttnBlockParams
       const f32x2 sc2 = {scale_log2, scale_log2};
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
-        const f32x2 lo = f32x2{sv[kt][0], sv[kt][1]} * sc2 + f32x2{bv[kt][0], bv[kt][1]};
-        const f32x2 hi = f32x2{sv[kt][2], sv[kt][3]} * sc2 + f32x2{bv[kt][2], bv[kt][3]};
+        const f32x2 lo = f32x2{sv[kt][0], sv[kt][1]} * sc2 + f32x2{bvu[h][kt][0], bvu[h][kt][1]};
+        const f32x2 hi = f32x2{sv[kt][2], sv[kt][3]} * sc2 + f32x2{bvu[h][kt][2], bvu[h][kt][3]};
         sv[kt] = f32x4{lo[0], lo[1], hi[0], hi[1]};
       }
       float mx = -INFINITY;
@@ -802,59 +814,67 @@ __global__ __launch_bounds__(512, 1) void swin_attn96_kernel(SwinAttnBlockParams
       for (int dt = 0; dt < 2; ++dt) {
         const f32x2 lo = f32x2{o[dt][0], o[dt][1]} * f32x2{inv, inv};
         const f32x2 hi = f32x2{o[dt][2], o[dt][3]} * f32x2{inv, inv};
-        u32x2 pk = {__builtin_bit_cast(unsigned, __builtin_convertvector(lo, bf16x2)),
-                    __builtin_bit_cast(unsigned, __builtin_convertvector(hi, bf16x2))};
-        *(EVT_LDS u32x2*)(L + AT96_O + (16 * qt + c16) * AT96_ROW + (32 * h + 16 * dt + 4 * g) * 2) = pk;
+        const u32x2 pk = {__builtin_bit_cast(unsigned, __builtin_convertvector(lo, bf16x2)),
+                          __builtin_bit_cast(unsigned, __builtin_convertvector(hi, bf16x2))};
+        *(EVT_LDS u32x2*)(L + AT96_XO + (16 * qt + c16) * AT96_ROW + (32 * h + 16 * dt + 4 * g) * 2) = pk;
       }
     }
-    __syncthreads();
-    // ---- P3: proj + bias + residual -> xm, row statistics (wave = token tile x 3 feature tiles) ----
+    // ---- P3: proj + bias + residual -> xm and its row statistics (token tile `wave`) ----
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's O rows are in LDS
     {
-      const int tt = wave & 3, ft0 = (wave >> 2) * 3;
+      const int t = 16 * qt + c16;
+      const int64_t row = G.row(min(t, 48));
+      bf16x4 xr[6];  // residual rows (L2-resident: read by this window's prefetch)
+#pragma unroll
+      for (int f = 0; f < 6; ++f) xr[f] = *(const bf16x4*)(x + row * 96 + 16 * f + 4 * g);
       u32x4 bo[3];
 #pragma unroll
       for (int ks = 0; ks < 3; ++ks)
-        bo[ks] = *(const EVT_LDS u32x4*)(L + AT96_O + (16 * tt + c16) * AT96_ROW + 64 * ks + 16 * g);
-      const int t = 16 * tt + c16;
-      const bool ok = t < 49;
-      const int64_t row = G.row(min(t, 48));
+        bo[ks] = *(const EVT_LDS u32x4*)(L + AT96_XO + t * AT96_ROW + 64 * ks + 16 * g);
       float s1 = 0.f, s2 = 0.f;
+      u32x2 ov[6];
 #pragma unroll
-      for (int f = 0; f < 3; ++f) {
-        const int ft = ft0 + f;
-        f32x4 acc = bpr[f];
+      for (int f = 0; f < 6; ++f) {
+        f32x4 acc = *(const EVT_LDS f32x4*)(L + AT96_CV + (288 + 16 * f + 4 * g) * 4);
 #pragma unroll
         for (int ks = 0; ks < 3; ++ks) {
-          const u32x4 wv = *(const EVT_LDS u32x4*)(L + AT96_WP + (16 * ft + c16) * AT96_ROW + 64 * ks + 16 * g);
+          const u32x4 wv = *(const EVT_LDS u32x4*)(L + AT96_WP + (16 * f + c16) * AT96_ROW + 64 * ks + 16 * g);
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wv),
                                                         __builtin_bit_cast(bf16x8, bo[ks]), acc, 0, 0, 0);
         }
-        const bf16x4 xr = *(const EVT_LDS bf16x4*)(L + AT96_XR + t * AT96_ROW + (16 * ft + 4 * g) * 2);
-        const f32x4 v = acc + f32x4{(float)xr[0], (float)xr[1], (float)xr[2], (float)xr[3]};
+        const f32x4 v = acc + f32x4{(float)xr[f][0], (float)xr[f][1], (float)xr[f][2], (float)xr[f][3]};
         const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-        if (ok) *(bf16x4*)((bf16*)p.xm + row * 96 + 16 * ft + 4 * g) = o;
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           const float fv = (float)o[jj];
           s1 += fv;
           s2 += fv * fv;
         }
+        ov[f] = __builtin_bit_cast(u32x2, o);
       }
       s1 += __shfl_xor(s1, 16, 64);
       s2 += __shfl_xor(s2, 16, 64);
       s1 += __shfl_xor(s1, 32, 64);
       s2 += __shfl_xor(s2, 32, 64);
-      if (g == 0) *(EVT_LDS f32x2*)(L + AT96_PART + ((wave >> 2) * 64 + t) * 8) = f32x2{s1, s2};
-    }
-    __syncthreads();
-    // ---- P4: row statistics of xm (two partials per token, fixed order) ----
-    if (tid < 49) {
-      const f32x2 a = *(const EVT_LDS f32x2*)(L + AT96_PART + tid * 8);
-      const f32x2 c = *(const EVT_LDS f32x2*)(L + AT96_PART + (64 + tid) * 8);
-      float* so = p.stats_out + G.row(tid) * 2 * p.nslots;
-      so[0] = a[0] + c[0];
-      so[1] = a[1] + c[1];
-      for (int k = 1; k < p.nslots; ++k) so[2 * k] = so[2 * k + 1] = 0.f;
+      // xm rows of this token tile staged over its (dead) O rows, then whole-row 16-B stores
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int f = 0; f < 6; ++f)
+        *(EVT_LDS u32x2*)(L + AT96_XO + t * AT96_ROW + (16 * f + 4 * g) * 2) = ov[f];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int idx = 64 * i + lane, r = idx / 12, j = idx - r * 12, tr = 16 * qt + r;
+        if (tr < 49) {
+          const u32x4 v = *(const EVT_LDS u32x4*)(L + AT96_XO + tr * AT96_ROW + j * 16);
+          store_b128((bf16*)p.xm + G.row(tr) * 96 + 8 * j, v);
+        }
+      }
+      if (g == 0 && t < 49) {
+        float* so = p.stats_out + row * 2 * p.nslots;
+        *(f32x2*)so = f32x2{s1, s2};
+        for (int k = 1; k < p.nslots; ++k) *(f32x2*)(so + 2 * k) = f32x2{0.f, 0.f};
+      }
     }
   }
 }
@@ -964,8 +984,8 @@ hipError_t swin_mlp96_launch(const SwinMlpParams& p, hipStream_t s) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, MLP96_LDS);
   }
   const int waves = (p.M + 31) / 32;
-  const int grid = std::max(1, std::min(ncu, (waves + 7) / 8));
-  hipLaunchKernelGGL(swin_mlp96_kernel, dim3(grid), dim3(512), MLP96_LDS, s, p);
+  const int grid = std::max(1, std::min(ncu, (waves + MLP96_WAVES - 1) / MLP96_WAVES));
+  hipLaunchKernelGGL(swin_mlp96_kernel, dim3(grid), dim3(64 * MLP96_WAVES), MLP96_LDS, s, p);
   return hipGetLastError();
 }
 
@@ -983,7 +1003,7 @@ hipError_t swin_attn96_launch(const SwinAttnBlockParams& p, hipStream_t s) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, AT96_LDS);
   }
   const int windows = p.B * (p.R / 7) * (p.R / 7);
-  hipLaunchKernelGGL(swin_attn96_kernel, dim3(std::min(windows, ncu)), dim3(512), AT96_LDS, s, p);
+  hipLaunchKernelGGL(swin_attn96_kernel, dim3(std::min(windows, 2 * ncu)), dim3(256), AT96_LDS, s, p);
   return hipGetLastError();
 }
 
