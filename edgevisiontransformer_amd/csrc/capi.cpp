@@ -1293,6 +1293,20 @@ int evt_swin_forward(evt_model* m, const float* img, int B, float* logits, void*
   // patch embed: Conv2d(k = s = patch) as im2col + Dense, then its LayerNorm -> stream x + stats
   int rows = B * s0.R * s0.R;
   const double es = (double)elem_size(dt);
+  const bool stem96 = dt == DT_BF16 && d.in_chans == 3 && d.patch_size == 4 && s0.C == 96 &&
+                      s0.Cst == 96 && m->patch.kpad == 64 && d.image_size % 16 == 0 &&
+                      d.image_size <= 256;
+  if (stem96) {  // Conv2d + embedding LayerNorm in one kernel (swin.hip, swin_embed96_kernel)
+    ProfScope ps(m, EVT_PROF_PATCH_EMBED, s);
+    prof_work(m, 2.0 * rows * 96 * 48,
+              (double)B * 3 * d.image_size * d.image_size * 4 + (double)rows * 96 * es +
+                  (double)rows * stats_slots(96) * 8);
+    SwinEmbedParams ep;
+    ep.img = img; ep.w = m->patch.w; ep.ldw = m->patch.kpad; ep.bias = m->patch.b;
+    ep.gamma = m->pnorm_g; ep.beta = m->pnorm_b; ep.x = m->x; ep.stats = m->sx;
+    ep.B = B; ep.S = d.image_size; ep.nslots = stats_slots(96); ep.eps = 1e-5f;
+    EVT_HIP(swin_embed96_launch(ep, s), "fused patch embedding");
+  } else {
   {
     ProfScope ps(m, EVT_PROF_PATCHIFY, s);
     prof_work(m, 0.0, (double)B * d.in_chans * d.image_size * d.image_size * 4 +
@@ -1310,6 +1324,7 @@ int evt_swin_forward(evt_model* m, const float* img, int B, float* logits, void*
     EVT_HIP(ln_rows_launch(dt, m->xm, s0.Cst, m->x, m->pnorm_g, m->pnorm_b, rows, s0.C, 1e-5f,
                            m->sx, stats_slots(s0.C), s),
             "patch norm");
+  }
   }
   for (size_t i = 0; i < m->stages.size(); ++i) {
     const SwinStage& st = m->stages[i];

@@ -215,6 +215,20 @@ struct SwinAttnBlockParams {
   float eps;
 };
 hipError_t swin_attn96_launch(const SwinAttnBlockParams& p, hipStream_t s);
+// fused Swin stem (swin.hip): Conv2d(3, 96, k = s = 4) + LayerNorm(96) -> bf16 stream + stats
+struct SwinEmbedParams {
+  const float* img;        // [B][3][S][S] fp32 NCHW
+  const void* w;           // packed patch weights [>= 96][ldw] bf16, k = (c, kh, kw), zero past 48
+  int64_t ldw;
+  const float* bias;       // [96]
+  const float* gamma;      // [96] embedding LayerNorm
+  const float* beta;       // [96]
+  void* x;                 // [B*(S/4)^2][96] bf16 stage-1 stream
+  float* stats;            // [rows][nslots][2] statistics of x (slot 0; the rest zeroed)
+  int B, S, nslots;
+  float eps;
+};
+hipError_t swin_embed96_launch(const SwinEmbedParams& p, hipStream_t s);
 int gemm_variant();  // the calling thread's evt_set_gemm_variant value (0 = automatic)
 bool gemm_variant_supported(int v);  // compiled into this build (lab variants: EVT_GEMM_LAB)
 

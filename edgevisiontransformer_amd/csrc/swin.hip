@@ -879,6 +879,148 @@ __global__ __launch_bounds__(256, 2) void swin_attn96_kernel(SwinAttnBlockParams
   }
 }
 
+// ---- fused patch embedding of the 3-channel, 4x4-patch, C = 96 stem (Swin-T / Swin-S) ---------
+// Conv2d(3, 96, k = s = 4) + the embedding LayerNorm(96) -> stage-1 stream x (bf16) and its row
+// statistics in one pass. The three-kernel path (im2col rows, the Dense GEMM writing the bf16
+// conv output, ln_rows_kernel reading it back) moves the 154 MB fp32 image plus 3 x 154 MB of
+// bf16 rows at bs256; this one reads the image and writes x.
+//   Persistent blocks (4 per CU) walk patch rows (image b, row py); the fp32 image strip
+//   [c][kh][S] of the NEXT patch row is loaded into registers while the current one is computed
+//   (coalesced 16-B loads), then written to LDS. Wave = token tile (16 patches); per tile
+//   C^T = W . P^T on v_mfma_f32_16x16x32_bf16 (K = 48 in two k-steps; the packed weight's K
+//   padding is zero, W in LDS with 144-B rows), the B operand built from two LDS float4 reads per
+//   lane (8 consecutive k = (c, kh, kw) are kh = 2q, 2q + 1 of one channel, 4 kw each). Conv output
+//   + bias stays fp32 into the LayerNorm (two-pass mean / variance over the token's 96 features:
+//   24 per lane, 4 lane groups); the stored bf16 values' (sum, sumsq) go to slot 0; x rows are
+//   staged in LDS and leave as whole 192-B rows.
+constexpr int EMB96_WROW = 144;  // W rows: 64 bf16 (48 + zero pad) + 16 B against bank conflicts
+constexpr int EMB96_XROW = 208;  // staged x rows: 96 bf16 + pad
+constexpr int EMB96_PF = 3;      // strip float4 per thread in flight (12 rows x S/4 <= 768)
+
+__global__ __launch_bounds__(256) void swin_embed96_kernel(SwinEmbedParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int S = p.S, R = S / 4, q4 = S / 4;
+  EVT_LDS char* ws = (EVT_LDS char*)smem;
+  EVT_LDS float* strip = (EVT_LDS float*)(smem + 96 * EMB96_WROW);  // [12][S]
+  EVT_LDS char* xs = (EVT_LDS char*)strip + 12 * S * 4;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c16 = lane & 15;
+  const int nrow = p.B * R;  // patch rows (b, py)
+  for (int e = tid; e < 96 * 8; e += 256) {
+    const int n = e >> 3, c = e & 7;
+    *(EVT_LDS u32x4*)(ws + n * EMB96_WROW + 16 * c) =
+        *(const u32x4*)((const bf16*)p.w + (int64_t)n * p.ldw + 8 * c);
+  }
+  f32x4 pf[EMB96_PF];
+  auto fetch = [&](int pr) {  // strip of patch row pr: row (c, kh) = img[b][c][4 py + kh][0 .. S)
+    const int b = pr / R, py = pr - b * R;
+#pragma unroll
+    for (int k = 0; k < EMB96_PF; ++k) {
+      const int e = tid + 256 * k, r = e / q4, i = e - r * q4;
+      if (r < 12) {
+        const int c = r >> 2, kh = r & 3;
+        pf[k] = *(const f32x4*)(p.img + (((int64_t)b * 3 + c) * S + 4 * py + kh) * S + 4 * i);
+      }
+    }
+  };
+  if ((int)blockIdx.x < nrow) fetch(blockIdx.x);
+  const float inv_d = 1.0f / 96.0f;
+  const int ntt = (R + 15) / 16;
+  for (int pr = blockIdx.x; pr < nrow; pr += gridDim.x) {
+    __syncthreads();  // the previous row's strip / staging readers are done
+#pragma unroll
+    for (int k = 0; k < EMB96_PF; ++k) {
+      const int e = tid + 256 * k;
+      if (e < 12 * q4) *(EVT_LDS f32x4*)(strip + 4 * e) = pf[k];  // [r][S] = e / q4, 4 (e % q4)
+    }
+    __syncthreads();
+    if (pr + (int)gridDim.x < nrow) fetch(pr + gridDim.x);  // lands during this row's compute
+    const int b = pr / R, py = pr - b * R;
+    for (int tt = wave; tt < ntt; tt += 4) {
+      const int j = 16 * tt + c16;  // this lane's patch (token) in the row
+      const bool ok = j < R;
+      u32x4 bx[2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int gq = 4 * ks + g;  // k = 8 gq .. 8 gq + 7: channel gq >> 1, kh 2 (gq & 1) + {0, 1}
+        bx[ks] = u32x4{0u, 0u, 0u, 0u};
+        if (gq < 6 && ok) {
+          const int r0 = (gq >> 1) * 4 + 2 * (gq & 1);
+          const f32x4 a0 = *(const EVT_LDS f32x4*)(strip + r0 * S + 4 * j);
+          const f32x4 a1 = *(const EVT_LDS f32x4*)(strip + (r0 + 1) * S + 4 * j);
+          bx[ks][0] = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a0[0], a0[1]}, bf16x2));
+          bx[ks][1] = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a0[2], a0[3]}, bf16x2));
+          bx[ks][2] = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a1[0], a1[1]}, bf16x2));
+          bx[ks][3] = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a1[2], a1[3]}, bf16x2));
+        }
+      }
+      f32x4 acc[6];
+#pragma unroll
+      for (int ft = 0; ft < 6; ++ft) {
+        acc[ft] = load4(p.bias + 16 * ft + 4 * g);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const u32x4 wv = *(const EVT_LDS u32x4*)(ws + (16 * ft + c16) * EMB96_WROW + 64 * ks + 16 * g);
+          acc[ft] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wv),
+                                                            __builtin_bit_cast(bf16x8, bx[ks]), acc[ft], 0, 0, 0);
+        }
+      }
+      // acc[ft][jj]: feature 16 ft + 4 g + jj of patch j; LayerNorm over the 96 features
+      float s = 0.f;
+#pragma unroll
+      for (int ft = 0; ft < 6; ++ft) s += (acc[ft][0] + acc[ft][1]) + (acc[ft][2] + acc[ft][3]);
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      const float mean = s * inv_d;
+      float v2 = 0.f;
+#pragma unroll
+      for (int ft = 0; ft < 6; ++ft)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) v2 += (acc[ft][jj] - mean) * (acc[ft][jj] - mean);
+      v2 += __shfl_xor(v2, 16, 64);
+      v2 += __shfl_xor(v2, 32, 64);
+      const float rstd = rsqrtf(v2 * inv_d + p.eps);
+      float s1 = 0.f, s2 = 0.f;
+      EVT_LDS char* xrow = xs + (16 * wave + c16) * EMB96_XROW;
+#pragma unroll
+      for (int ft = 0; ft < 6; ++ft) {
+        const f32x4 gm = load4(p.gamma + 16 * ft + 4 * g), bt = load4(p.beta + 16 * ft + 4 * g);
+        const f32x4 y = (acc[ft] - mean) * rstd * gm + bt;
+        const bf16x4 o = {(bf16)y[0], (bf16)y[1], (bf16)y[2], (bf16)y[3]};
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const float f = (float)o[jj];
+          s1 += f;
+          s2 += f * f;
+        }
+        *(EVT_LDS bf16x4*)(xrow + (16 * ft + 4 * g) * 2) = o;
+      }
+      s1 += __shfl_xor(s1, 16, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      const int64_t row0 = ((int64_t)b * R + py) * R + 16 * tt;  // stream row of patch 16 tt
+      if (g == 0 && ok) {
+        float* st = p.stats + (row0 + c16) * 2 * p.nslots;
+        *(f32x2*)st = f32x2{s1, s2};
+        for (int k = 1; k < p.nslots; ++k) *(f32x2*)(st + 2 * k) = f32x2{0.f, 0.f};
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // the wave's 16 staged rows leave as whole 192-B rows (12 lanes x 16 B each)
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int idx = 64 * i + lane, r = idx / 12, c = idx - r * 12;
+        if (16 * tt + r < R) {
+          const u32x4 v = *(const EVT_LDS u32x4*)(xs + (16 * wave + r) * EMB96_XROW + 16 * c);
+          store_b128((bf16*)p.x + (row0 + r) * 96 + 8 * c, v);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging reads done before reuse
+    }
+  }
+}
+
 template <typename T, int LPR, int NC>
 hipError_t ln_rows_lc(const void* x, int64_t ld, void* y, const float* g, const float* bb,
                       int rows, int D, float eps, float* stats, int nslots, hipStream_t s) {
@@ -1004,6 +1146,23 @@ hipError_t swin_attn96_launch(const SwinAttnBlockParams& p, hipStream_t s) {
   }
   const int windows = p.B * (p.R / 7) * (p.R / 7);
   hipLaunchKernelGGL(swin_attn96_kernel, dim3(std::min(windows, 2 * ncu)), dim3(256), AT96_LDS, s, p);
+  return hipGetLastError();
+}
+
+hipError_t swin_embed96_launch(const SwinEmbedParams& p, hipStream_t s) {
+  if (p.B <= 0) return hipSuccess;
+  if (p.S % 16 || 3 * p.S > 256 * EMB96_PF || p.ldw < 64 || p.ldw % 8 || p.nslots < 1 ||
+      p.nslots > 4)
+    return hipErrorInvalidValue;
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  const size_t lds = (size_t)96 * EMB96_WROW + 12 * p.S * 4 + 64 * EMB96_XROW;
+  const int rows = p.B * (p.S / 4);
+  hipLaunchKernelGGL(swin_embed96_kernel, dim3(std::min(rows, 4 * ncu)), dim3(256), lds, s, p);
   return hipGetLastError();
 }
 
