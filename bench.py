@@ -73,8 +73,9 @@ def parse():
     ap.add_argument("--gemm-variant", type=int, default=0, help="evt_set_gemm_variant (tuning A/B)")
     ap.add_argument("--isolated-probe", action="store_true",
                     help="also time FC1 alone, back to back (reported as roofline.isolated_probe_us)")
-    ap.add_argument("--fusion", type=int, default=0,
-                    help="evt_model_set_fusion flags (0 = separate kernels, 1 = fused QKV + attention)")
+    ap.add_argument("--fusion", type=int, default=-1,
+                    help="evt_model_set_fusion flags (-1 = the library default: 2 = chained GEMM "
+                         "launches; 0 = separate kernels; 1 = fused QKV + attention)")
     ap.add_argument("--probe-only", type=int, default=0, metavar="N",
                     help="only launch the FC1 probe kernel N times and exit (PMC collection)")
     ap.add_argument("--global-batch", type=int, default=0,
@@ -224,7 +225,7 @@ def main():
     else:
         B, G, cap = args.batch, world * args.batch, args.batch
     model = mod.build_named(args.model, dtype=args.dtype, seed=0, max_batch=cap)
-    if args.fusion:
+    if args.fusion >= 0:
         model.set_fusion(args.fusion)
     if args.gemm_variant:
         from edgevisiontransformer_amd import _lib

@@ -28,6 +28,7 @@ EPI_BIAS, EPI_GELU, EPI_RESID, EPI_POS, EPI_OUT_F32 = 1, 2, 4, 8, 16
 EPI_LNIN, EPI_RESLN, EPI_STATS, EPI_GELU_ERF = 32, 64, 128, 256
 EPI_OUT_MX8 = 512
 FUSE_QKV_ATTENTION = 1  # evt_model_set_fusion flag (include/evt.h EVT_FUSE_QKV_ATTENTION)
+FUSE_GEMM_CHAIN = 2  # evt_model_set_fusion flag (EVT_FUSE_GEMM_CHAIN: out-proj -> FC1, default on)
 # evt_model_profile roles (include/evt.h EVT_PROF_*)
 PROF_ROLES = ("patchify", "patch_embed", "qkv", "attention", "out_proj", "fc1", "fc2", "head",
               "qkv_attention", "t2t_unfold", "t2t_kqv", "t2t_performer", "merge", "attn_sublayer",

@@ -144,6 +144,8 @@ struct evt_model {
   size_t hbuf_bytes = 0;
   void* hh = nullptr;        // [B, head_st]
   void* sk = nullptr;        // stream-K scratch of the model's GEMMs (gemm_sk_bytes)
+  unsigned* chain = nullptr; // hand-off words of chained GEMM launches (gemm_chain_launch)
+  size_t chain_bytes = 0;
   // Swin (family 2)
   evt_swin_desc sdesc{};
   std::vector<SwinStage> stages;
@@ -153,7 +155,7 @@ struct evt_model {
   hipGraph_t graph = nullptr;        // evt_graph_capture
   hipGraphExec_t graph_exec = nullptr;
   // evt_model_profile: HIP events around every launch of the last forward, by role
-  int fusion = 0;                    // evt_model_set_fusion (opt-in)
+  int fusion = EVT_FUSE_GEMM_CHAIN;  // evt_model_set_fusion
   bool prof = false;
   std::vector<hipEvent_t> prof_ev;   // pool (pairs)
   std::vector<int> prof_role;        // role of pair i of the last forward
@@ -377,8 +379,7 @@ void dense_work(const evt_model* m, const DenseW& w, const DenseCall& c) {
   prof_work(m, 2.0 * M * K * N, bytes);
 }
 
-int dense(const evt_model* m, const DenseW& w, const DenseCall& c, hipStream_t s) {
-  dense_work(m, w, c);
+GemmParams dense_params(const evt_model* m, const DenseW& w, const DenseCall& c) {
   GemmParams p{};
   p.A = c.A;
   p.lda = c.lda;
@@ -412,8 +413,29 @@ int dense(const evt_model* m, const DenseW& w, const DenseCall& c, hipStream_t s
   p.nslots = stats_slots(c.slot_width ? c.slot_width : width);
   p.stats_step = c.stats_step;
   gemm_sk_bind(m->sk, p);
+  return p;
+}
+
+int dense(const evt_model* m, const DenseW& w, const DenseCall& c, hipStream_t s) {
+  dense_work(m, w, c);
+  const GemmParams p = dense_params(m, w, c);
   EVT_HIP(gemm_launch(m->dtype, c.flags, p, s), "dense");
   return EVT_OK;
+}
+
+// Producer Dense (out-proj) and the consumer Dense reading its output (FC1) as one chained
+// persistent launch where it qualifies (gemm_chain_launch), else the two launches.
+int dense_pair(const evt_model* m, const DenseW& wa, const DenseCall& ca, const DenseW& wb,
+               const DenseCall& cb, hipStream_t s) {
+  if (!m->prof && m->chain && (m->fusion & EVT_FUSE_GEMM_CHAIN)) {
+    const GemmParams pa = dense_params(m, wa, ca), pb = dense_params(m, wb, cb);
+    const hipError_t e =
+        gemm_chain_launch(m->dtype, ca.flags, pa, cb.flags, pb, m->chain, m->chain_bytes, s);
+    if (e == hipSuccess) return EVT_OK;
+    if (e != hipErrorNotSupported) EVT_HIP(e, "chained dense");
+  }
+  EVT_RC(dense(m, wa, ca, s));
+  return dense(m, wb, cb, s);
 }
 
 
@@ -474,6 +496,9 @@ int alloc_encoder_ws(evt_model* m, int B, size_t hbuf_bytes, hipStream_t s) {
   EVT_RC(dev_alloc(m, &m->o, rows * m->sh.max_inner * es));
   EVT_RC(dev_alloc(m, &m->hbuf, hbuf_bytes));
   m->hbuf_bytes = hbuf_bytes;
+  m->chain_bytes = ((rows + 255) / 256 + 3) * 4 + 16;
+  EVT_RC(dev_alloc(m, (void**)&m->chain, m->chain_bytes));
+  EVT_HIP(hipMemsetAsync(m->chain, 0, m->chain_bytes, s), "memset chain words");
   return EVT_OK;
 }
 
@@ -496,6 +521,8 @@ int dense_head(const evt_model* m, const DenseW& w, const DenseCall& c, hipStrea
 }
 
 // Encoder layers (transformer_encoder.py:13-18 / :26-34) on the token stream m->x (+ stats sx).
+// Out-proj -> FC1 run as one chained launch where it qualifies (dense_pair; EVT_FUSE_GEMM_CHAIN,
+// on by default).
 int run_encoder(evt_model* m, int B, hipStream_t s) {
   const int D = m->D, T = m->sh.T, rows = B * T;
   const float log2e = 1.4426950408889634f;
@@ -529,23 +556,27 @@ int run_encoder(evt_model* m, int B, hipStream_t s) {
       AttnParams ap{m->qkv, 3 * L.inner, m->o, L.inner, T, L.heads, B, 0.125f * log2e};
       EVT_HIP(attention_launch(m->dtype, ap, s), "attention");
     }
-    {  // out-proj + bias + LN1(x) residual -> xm (+ stats); STANDARD: + x
-      ProfScope ps(m, EVT_PROF_OUT_PROJ, s);
-      DenseCall c;
-      c.flags = m->standard ? (EPI_BIAS | EPI_RESID | EPI_STATS)
-                            : (EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS);
-      c.A = m->o; c.lda = L.inner; c.C = m->xm; c.ldc = D; c.M = rows; c.N = D;
-      c.resid = m->x; c.ldr = D; c.rstats = m->sx; c.rgamma = L.ln1_g; c.rbeta = L.ln1_b;
-      c.stats_out = m->sm;
-      EVT_RC(dense(m, L.out, c, s));
-    }
-    {  // LN2-folded FC1 + GELU (ffn.py:8; STANDARD: exact erf GELU)
+    // out-proj + bias + LN1(x) residual -> xm (+ stats); STANDARD: + x
+    DenseCall co;
+    co.flags = m->standard ? (EPI_BIAS | EPI_RESID | EPI_STATS)
+                           : (EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS);
+    co.A = m->o; co.lda = L.inner; co.C = m->xm; co.ldc = D; co.M = rows; co.N = D;
+    co.resid = m->x; co.ldr = D; co.rstats = m->sx; co.rgamma = L.ln1_g; co.rbeta = L.ln1_b;
+    co.stats_out = m->sm;
+    // LN2-folded FC1 + GELU (ffn.py:8; STANDARD: exact erf GELU)
+    DenseCall c1;
+    c1.flags = EPI_LNIN | EPI_BIAS | (m->standard ? EPI_GELU_ERF : EPI_GELU);
+    c1.A = m->xm; c1.lda = D; c1.C = m->hbuf; c1.ldc = L.ffn_st; c1.M = rows; c1.N = L.ffn_st;
+    c1.stats_in = m->sm;
+    if (!m->prof) {  // chained where it qualifies (one role per bracketed launch when profiling)
+      EVT_RC(dense_pair(m, L.out, co, L.fc1, c1, s));
+    } else {
+      {
+        ProfScope ps(m, EVT_PROF_OUT_PROJ, s);
+        EVT_RC(dense(m, L.out, co, s));
+      }
       ProfScope ps(m, EVT_PROF_FC1, s);
-      DenseCall c;
-      c.flags = EPI_LNIN | EPI_BIAS | (m->standard ? EPI_GELU_ERF : EPI_GELU);
-      c.A = m->xm; c.lda = D; c.C = m->hbuf; c.ldc = L.ffn_st; c.M = rows; c.N = L.ffn_st;
-      c.stats_in = m->sm;
-      EVT_RC(dense(m, L.fc1, c, s));
+      EVT_RC(dense(m, L.fc1, c1, s));
     }
     {  // FC2 + bias + LN2(xm) residual -> x (+ stats); STANDARD: + xm
       ProfScope ps(m, EVT_PROF_FC2, s);
@@ -1458,7 +1489,8 @@ int evt_patch_merge(int dtype, const void* x, int64_t ldx, int B, int R, int C, 
 
 int evt_model_set_fusion(evt_model* m, int flags) {
   if (!m) return fail(EVT_EINVAL, "model is NULL");
-  if (flags & ~EVT_FUSE_QKV_ATTENTION) return fail(EVT_EINVAL, "unknown fusion flag");
+  if (flags & ~(EVT_FUSE_QKV_ATTENTION | EVT_FUSE_GEMM_CHAIN))
+    return fail(EVT_EINVAL, "unknown fusion flag");
   m->fusion = flags;
   return EVT_OK;
 }

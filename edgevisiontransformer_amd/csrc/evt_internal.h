@@ -58,6 +58,12 @@ constexpr int PAD_K = 64;   // K granularity (elements) of every packed operand
 constexpr int PAD_N = 64;   // column granularity of activation buffers
 
 hipError_t gemm_launch(int dtype, int flags, const GemmParams& p, hipStream_t s);
+// Producer (fa: out-proj with the LN residual and row statistics) and consumer (fb: the LN-
+// folded FC1 + GELU reading the producer's output) in one persistent launch with per-panel
+// hand-off words in sync (>= panels + 3 words, zero when allocated; every launch leaves them
+// zeroed). hipErrorNotSupported: launch them separately.
+hipError_t gemm_chain_launch(int dtype, int fa, const GemmParams& pa, int fb, const GemmParams& pb,
+                             unsigned* sync, size_t sync_bytes, hipStream_t s);
 // Skinny GEMM (small M, long K: the classifier head) as S K-splits in one launch, fp32 partials
 // part[S][M][ntiles*128], then a fixed-order reduction + bias (+ GELU) into C (deterministic).
 // flags: EPI_BIAS and/or EPI_GELU and/or EPI_OUT_F32 only; K % (S * 64) == 0.

@@ -1204,7 +1204,16 @@ __device__ __forceinline__ void pers_resid_early(const GemmParams& p, int wm, in
   }
 }
 
-template <int FL, int DBG = 0, bool PADN = true, int ER = 0>
+// SC1: chained-launch producer (gemm_chain_kernel): every output byte is stored write-through
+// (sc1: 16-B buffer stores with aux 16, the 8-B row statistics as agent-scope atomic stores) so
+// that a consumer workgroup on another XCD reads it after its agent-scope acquire; otherwise
+// the outputs are non-temporal.
+__device__ __forceinline__ void stats_store_sc1(float* p, f32x2 v) {
+  __hip_atomic_store((unsigned long long*)p, __builtin_bit_cast(unsigned long long, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int FL, int DBG = 0, bool PADN = true, int ER = 0, bool SC1 = false>
 __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
                                               int wave, int wm, int wn, int m0, int n0, int tn,
                                               int lane, bool interior, int iter = 0,
@@ -1425,8 +1434,8 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
           svo = ((pos_orow(m0 + wm * 128 + 32 * k + 8 * i + rrow, p.P) - orow0) * (int)p.ldc +
                  wn * 64 + rch * 8) * 2;
         }
-        if (keep)  // nontemporal (aux nt): whole lines streamed past L2
-          buffer_store_b128<2>(v, cs, svo, so);
+        if (keep)  // nontemporal (aux nt): whole lines streamed past L2; SC1: write-through
+          buffer_store_b128<SC1 ? 16 : 2>(v, cs, svo, so);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
@@ -1452,31 +1461,86 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
         const int m = m0 + rl + 32 * k;
         const f32x2 o = part[rl + 32 * k];
         const int sm = (FL & EPI_POS) ? pos_orow(m, p.P) : m;
-        if (interior || m < p.M)
-          *(f32x2*)(p.stats_out + 2 * ((int64_t)p.nslots * sm + 2 * tn + (wn >> 1))) = st[k] + o;
+        if (interior || m < p.M) {
+          float* so = p.stats_out + 2 * ((int64_t)p.nslots * sm + 2 * tn + (wn >> 1));
+          if constexpr (SC1)
+            stats_store_sc1(so, st[k] + o);
+          else
+            *(f32x2*)so = st[k] + o;
+        }
       }
     }
   }
 }
 
-template <int FL, int DBG = 0, bool PADN = true>
-__global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int total) {
+// Chained launches (gemm_chain_kernel): a producer GEMM's tiles, then a consumer GEMM whose M
+// panel p may start once the producer's tiles of panel p are stored. ChainCtx is the block's view
+// of the hand-off words (zeroed by the launch): cnt[p] = producer tiles of panel p published,
+// gdone = producer tiles published in all, err = a bounded wait gave up.
+struct ChainCtx {
+  unsigned* cnt = nullptr;
+  unsigned* gdone = nullptr;
+  unsigned* err = nullptr;
+  unsigned need = 0;    // producer tiles per panel
+  unsigned totalA = 0;  // producer tiles
+  bool all_ready = false;
+};
+
+constexpr int CHAIN_WORD = PERS_LDS;  // LDS broadcast word (the kernels allocate PERS_LDS + 16)
+
+// Producer: publish panel tm (one lane; every storing wave's stores of it are complete).
+__device__ __forceinline__ void chain_publish(const ChainCtx& cx, int tm) {
+  __hip_atomic_fetch_add(cx.cnt + tm, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_add(cx.gdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Consumer: wait (all threads, block-uniform) until panel tm is published, then one agent-scope
+// acquire; once an acquire has followed the observation that every producer tile is published,
+// later tiles need neither. Bounded (~1 s): on timeout the err word is set and the block goes on.
+__device__ __forceinline__ void chain_wait(ChainCtx& cx, int tm, char* smem) {
+  if (cx.all_ready) return;
+  if (threadIdx.x == 0) {
+    bool ok = false;
+    for (int i = 0; i < (1 << 23); ++i) {
+      if (__hip_atomic_load(cx.cnt + tm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= cx.need) {
+        ok = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (!ok) __hip_atomic_store(cx.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned d = __hip_atomic_load(cx.gdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *(EVT_LDS int*)(smem + CHAIN_WORD) = (d >= cx.totalA) ? 1 : 0;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    wait_vmcnt0();
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  big8_bar();
+  cx.all_ready = __builtin_amdgcn_readfirstlane(*(const EVT_LDS int*)(smem + CHAIN_WORD)) != 0;
+}
+
+// The persistent tile walk of one GEMM from logical tile `tile` in steps of gridDim.x.
+// ROLE 0: a plain launch; 1: chain producer (outputs write-through, each tile's panel published
+// one tile later, when every wave's stores of it have provably completed, the last one after a
+// drain); 2: chain consumer (each tile's prologue waits for its panel).
+template <int FL, int DBG, bool PADN, int ROLE>
+__device__ __forceinline__ void pers_run(const GemmParams& p, int total, int tile, char* smem,
+                                         ChainCtx& cx) {
   // a quarter of the residual before the last K-tile (out-proj 160 -> 153 us); DBG 20: A/B without
   constexpr int ER = ((FL & EPI_RESID) != 0 && DBG != 7 && DBG != 20 && DBG != 18)
                          ? (DBG == 21 ? 1 : 2) : 0;  // DBG 21: A/B with one quarter
-  __shared__ __attribute__((aligned(16))) char smem[PERS_LDS];
+  constexpr bool SC1 = ROLE == 1;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
-  const int G = gridDim.x;  // XCD-aware order when a multiple of 8
-  int tile = (G & 7) ? (int)blockIdx.x : (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
-  if (tile >= total) return;
+  const int G = gridDim.x;
   const int nk = p.K / 64;
   int tm = tile / p.ntiles, tn = tile - tm * p.ntiles;
   if (DBG == 5) {  // experiment: stagger the blocks' start
     const int q = (blockIdx.x >> 3) & 3;
     for (int i = 0; i < q * nk; ++i) __builtin_amdgcn_s_sleep(20);
   }
+  if constexpr (ROLE == 2) chain_wait(cx, tm, smem);
   pers_coop_dma<FL>(p, smem, wave, lane, tm * BIG_BM, tn * BIG_BN);
   big8_prologue(p, smem, wave, lane, tm * BIG_BM, tn * BIG_BN, nk);
   wait_vmcnt0();  // the first K-tile's waits assume PERS_X younger VMEM ops or a drain
@@ -1484,6 +1548,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
   // nk >= 3: per-tile LayerNorm coefficients / next statistics DMA inside the main loop
   const bool early = nk >= 3 && DBG != 16 && DBG != 17;
   int iter = 0;
+  int pub_tm = -1;  // ROLE 1: the previous tile's panel, published during this tile
   auto stamp = [&](int k) {  // DBG 3: timeline of block's tiles (s_memtime, wave 0)
     if ((DBG == 3 || DBG == 5) && tid == 0 && iter < 16)
       ((unsigned long long*)p.pos)[((int64_t)blockIdx.x * 16 + iter) * 8 + k] = __builtin_amdgcn_s_memtime();
@@ -1506,9 +1571,11 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
       ntm = next / p.ntiles;
       ntn = next - ntm * p.ntiles;
     }
+    // ROLE 2: the next tile's operands may be fetched ahead only once every panel is known ready
+    const bool rdy = ROLE != 2 || cx.all_ready;
     // the next tile's prologue rides in the last K-tiles' idle DMA slots (big8_ktile) as K-tiles
     // nk, nk + 1 of one stream: for odd nk the next tile starts at the other buffer parity
-    const bool cont = has_next && nk >= 2 && DBG != 16 && (DBG != 6 || !(nk & 1));
+    const bool cont = has_next && rdy && nk >= 2 && DBG != 16 && (DBG != 6 || !(nk & 1));
     const int npar = cont ? par ^ (nk & 1) : 0;
     auto last = [&]() {
       if constexpr (ER > 0) pers_resid_early<0, 1>(p, wm, wn, ln, m0, n0, rre);
@@ -1522,7 +1589,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
       // free once those coefficients are read: every later phase retires group 1's LDS ops)
       auto pre1 = [&]() { pers_coef<FL>(p, smem, tid - 256); };
       auto mid = [&]() {
-        if (has_next) pers_coop_dma<FL>(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN);
+        if (has_next && rdy) pers_coop_dma<FL>(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN);
       };
       if constexpr (DBG == 18)  // A/B: groups re-synchronised before the epilogue
         big8_loop<PERS_X>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
@@ -1533,7 +1600,15 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
                                                    ntm * BIG_BM, ntn * BIG_BN, pre1, mid, last,
                                                    last3, par);
       stamp(1);
-      if (has_next && !cont) big8_prologue(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nk);
+      if (has_next && !cont) {
+        if constexpr (ROLE == 2) {
+          if (!rdy) {  // before every panel is known ready: wait, then the skipped DMAs
+            chain_wait(cx, ntm, smem);
+            pers_coop_dma<FL>(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN);
+          }
+        }
+        big8_prologue(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nk);
+      }
     } else {
       big8_loop<PERS_X, false, NoOp, NoOp, (ER > 0 ? 4 : 0), decltype(last), (ER > 1 ? 4 : 0),
                 decltype(last3)>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
@@ -1543,6 +1618,9 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       big8_bar();
       if (has_next) {
+        if constexpr (ROLE == 2) {
+          if (!rdy) chain_wait(cx, ntm, smem);
+        }
         pers_coop_dma<FL>(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN);
         if (!cont) big8_prologue(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nk);
       }
@@ -1550,12 +1628,18 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     stamp(2);
+    // ROLE 1: every wave passed this tile's K-tile-1 waits (vmcnt <= 8 with more than 8 younger
+    // DMAs) before the barriers wave 0 has crossed since: the previous tile's stores are complete
+    if constexpr (ROLE == 1) {
+      if (pub_tm >= 0 && tid == 0) chain_publish(cx, pub_tm);
+      pub_tm = tm;
+    }
     const bool interior = (m0 + BIG_BM <= p.M) && (n0 + BIG_BN <= p.N);
     if constexpr (DBG == 6)  // A/B: the round-1 epilogue
       pers_epilogue_v1<FL, 0, PADN>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior);
     else
-      pers_epilogue<FL, DBG, PADN, ER>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior, iter,
-                                       rre, npar);
+      pers_epilogue<FL, DBG, PADN, ER, SC1>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior,
+                                            iter, rre, npar);
     stamp(7);
     ++iter;
     if (!has_next) break;
@@ -1564,6 +1648,61 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
     tile = next;
     tm = ntm;
     tn = ntn;
+  }
+  if constexpr (ROLE == 1) {  // the last tile: drain every wave, then publish
+    wait_vmcnt0();
+    big8_bar();
+    if (tid == 0) chain_publish(cx, pub_tm);
+  }
+}
+
+template <int FL, int DBG = 0, bool PADN = true>
+__global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int total) {
+  __shared__ __attribute__((aligned(16))) char smem[PERS_LDS];
+  const int G = gridDim.x;  // XCD-aware order when a multiple of 8
+  const int tile = (G & 7) ? (int)blockIdx.x : (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  if (tile >= total) return;
+  ChainCtx cx;
+  pers_run<FL, DBG, PADN, 0>(p, total, tile, smem, cx);
+}
+
+// Two dependent GEMMs in one persistent launch: producer FA (out-proj: LN residual, row
+// statistics) over every M panel, then consumer FB (FC1: LN-folded A = the producer's output) in
+// the same tile walk, so the CUs the producer's last, partial tile round
+// leaves idle start consumer tiles of panels that are already done (per-panel hand-off, acquire
+// at the consumer; DESIGN.md "Chained GEMM launches"). Every block is resident (one per CU) and
+// waits only on tiles of lower walk index, so the walk always progresses; waits are bounded.
+template <int FA, int FB>
+__global__ __launch_bounds__(512, 2) void gemm_chain_kernel(GemmParams pa, GemmParams pb,
+                                                            int totalA, int totalB,
+                                                            unsigned* sync) {
+  __shared__ __attribute__((aligned(16))) char smem[PERS_LDS + 16];
+  const int G = gridDim.x;  // multiple of 8, <= totalA (host)
+  const int lb = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  const int panels = (pa.M + BIG_BM - 1) / BIG_BM;
+  ChainCtx cx;
+  cx.cnt = sync;
+  cx.gdone = sync + panels;
+  cx.err = sync + panels + 1;
+  cx.need = (unsigned)pa.ntiles;
+  cx.totalA = (unsigned)totalA;
+  if (lb < totalA) pers_run<FA, 0, false, 1>(pa, totalA, lb, smem, cx);
+  int g = lb;
+  if (g < totalA) g += ((totalA - lb + G - 1) / G) * G;  // first walk index past the producer
+  if (g - totalA < totalB) pers_run<FB, 0, false, 2>(pb, totalB, g - totalA, smem, cx);
+  // self-cleaning hand-off words: the last block to finish (every other block is past its last
+  // poll) zeroes the counters for the next chained launch; err stays set
+  unsigned* fin = sync + panels + 2;
+  if (threadIdx.x == 0) {
+    wait_vmcnt0();
+    const unsigned old = __hip_atomic_fetch_add(fin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *(EVT_LDS unsigned*)(smem + CHAIN_WORD) = old == (unsigned)G - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (*(const EVT_LDS unsigned*)(smem + CHAIN_WORD)) {
+    for (int i = threadIdx.x; i < panels + 1; i += blockDim.x)
+      __hip_atomic_store(sync + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(fin, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1823,6 +1962,25 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Chained producer -> consumer launch (gemm_chain_kernel). hipErrorNotSupported when the pair
+// does not qualify (the caller then launches the two GEMMs separately).
+template <int FA, int FB>
+hipError_t launch_chain(const GemmParams& pa, const GemmParams& pb, unsigned* sync,
+                        size_t sync_bytes, hipStream_t s) {
+  GemmParams qa = pa, qb = pb;
+  qa.ntiles = (pa.ntiles * GEMM_BN) / BIG_BN;
+  qb.ntiles = (pb.ntiles * GEMM_BN) / BIG_BN;
+  const int panels = (pa.M + BIG_BM - 1) / BIG_BM;
+  const int totalA = panels * qa.ntiles, totalB = panels * qb.ntiles;
+  const int G = num_cus() & ~7;
+  // sync: [panels] counters, gdone, err, fin; zero at allocation, left zeroed by every launch
+  if (G < 8 || totalA < G || (size_t)(panels + 3) * 4 > sync_bytes)
+    return hipErrorNotSupported;
+  hipLaunchKernelGGL((gemm_chain_kernel<FA, FB>), dim3(G), dim3(512), 0, s, qa, qb, totalA, totalB,
+                     sync);
+  return hipGetLastError();
+}
+
 constexpr int SK_MAX_G = 256;
 
 int sk_grid() { return min(num_cus(), SK_MAX_G) & ~7; }
@@ -1998,6 +2156,18 @@ size_t gemm_sk_bytes() { return 4096 + (size_t)SK_MAX_G * SK_SLOT_FLOATS * sizeo
 void gemm_sk_bind(void* ws, GemmParams& p) {
   p.sk_flags = ws ? (int*)ws : nullptr;
   p.sk_part = ws ? (float*)((char*)ws + 4096) : nullptr;
+}
+
+hipError_t gemm_chain_launch(int dtype, int fa, const GemmParams& pa, int fb, const GemmParams& pb,
+                             unsigned* sync, size_t sync_bytes, hipStream_t s) {
+  constexpr int RES = EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS;
+  if (dtype != DT_BF16 || g_gemm_variant != 0 || fa != RES || !sync) return hipErrorNotSupported;
+  if (pa.M != pb.M || pa.N % BIG_BN || pb.N % BIG_BN || pa.K / 64 < 3 || pb.K / 64 < 3 ||
+      !use_pers(pa, fa) || !use_pers(pb, fb))
+    return hipErrorNotSupported;
+  if (fb == (EPI_LNIN | EPI_BIAS | EPI_GELU))
+    return launch_chain<RES, EPI_LNIN | EPI_BIAS | EPI_GELU>(pa, pb, sync, sync_bytes, s);
+  return hipErrorNotSupported;
 }
 
 hipError_t gemm_launch(int dtype, int flags, const GemmParams& p, hipStream_t s) {

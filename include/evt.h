@@ -157,12 +157,17 @@ int evt_model_profile_read(evt_model* m, float* us, int* launches);
  * role's time for the MFMA and HBM roofline fractions. */
 int evt_model_profile_work(evt_model* m, double* gflop, double* gbytes);
 
-/* Fused-kernel switches of ONE model handle (default 0 = the separate QKV GEMM + attention
- * kernels): EVT_FUSE_QKV_ATTENTION runs each bf16 ViT layer's LN1-folded QKV Dense and attention
- * core as one kernel (evt_qkv_attention) where the token count allows. Opt-in: measured slower
- * than the separate kernels at DeiT-base bs512 ("Fused QKV + attention"). Takes effect
- * at the next forward / graph capture of that handle; other handles are unaffected. */
+/* Fused-kernel switches of ONE model handle (default EVT_FUSE_GEMM_CHAIN):
+ * EVT_FUSE_QKV_ATTENTION runs each bf16 ViT layer's LN1-folded QKV Dense and attention core as
+ * one kernel (evt_qkv_attention) where the token count allows. Opt-in: measured slower than the
+ * separate kernels at DeiT-base bs512 ("Fused QKV + attention").
+ * EVT_FUSE_GEMM_CHAIN runs each bf16 ViT layer's out-proj -> FC1 as one chained persistent launch
+ * where the shapes allow (FC1 tiles start on the CUs the out-proj's last tile round leaves idle;
+ * bitwise the same results; DESIGN.md, "Chained GEMM launches"). Not used while the handle is
+ * profiling (evt_model_profile brackets one role per launch).
+ * Takes effect at the next forward / graph capture of that handle; other handles are unaffected. */
 #define EVT_FUSE_QKV_ATTENTION 1
+#define EVT_FUSE_GEMM_CHAIN 2
 int evt_model_set_fusion(evt_model* m, int flags);
 
 /* Pack a Keras [K, N] fp32 kernel into the GEMM operand layout Wp[Npad][Kpad] (dtype), zero
