@@ -143,9 +143,19 @@ __global__ __launch_bounds__(256) void patchify_cm_kernel(const float* __restric
   const int hh = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int np = HW / ps;
   const int per_c = ps * HW;
-  for (int c = 0; c < C; ++c) {
-    const float* src = img + (((int64_t)b * C + c) * HW + (int64_t)hh * ps) * HW;
-    for (int i = tid * 4; i < per_c; i += 256 * 4) *(f32x4*)(strip + c * per_c + i) = load4(src + i);  // LDS
+  if (per_c % 256 == 0) {  // every strip load straight to LDS (global_load_lds), one wait
+    const int wave = tid >> 6, lane = tid & 63;
+    for (int c = 0; c < C; ++c) {
+      const float* src = img + (((int64_t)b * C + c) * HW + (int64_t)hh * ps) * HW;
+      for (int i0 = wave * 256; i0 < per_c; i0 += 1024)
+        glds16(src + i0 + lane * 4, (EVT_LDS char*)smem + (c * per_c + i0) * 4);
+    }
+    wait_vmcnt0();
+  } else {
+    for (int c = 0; c < C; ++c) {
+      const float* src = img + (((int64_t)b * C + c) * HW + (int64_t)hh * ps) * HW;
+      for (int i = tid * 4; i < per_c; i += 256 * 4) *(f32x4*)(strip + c * per_c + i) = load4(src + i);  // LDS
+    }
   }
   __syncthreads();
   const int pd = ps * ps * C;
