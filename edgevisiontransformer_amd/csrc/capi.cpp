@@ -1364,14 +1364,40 @@ int evt_swin_forward(evt_model* m, const float* img, int B, float* logits, void*
     if (i > 0) {  // PatchMerging: gather -> LN(4C)-folded reduction -> stream x (+ stats)
       const SwinStage& pv = m->stages[i - 1];
       ProfScope ps(m, EVT_PROF_MERGE, s);
-      prof_work(m, 0.0, 2.0 * rows * 4 * pv.C * es + (double)rows * stats_slots(C) * 8);
-      EVT_HIP(merge_launch(dt, m->x, pv.Cst, B, pv.R, pv.C, m->hbuf, m->sm, stats_slots(C), s),
-              "patch merge");
       DenseCall c;
       c.flags = EPI_LNIN | EPI_BIAS | EPI_STATS;
-      c.A = m->hbuf; c.lda = 4 * pv.C; c.C = m->x; c.ldc = Cst; c.M = rows; c.N = Cst;
+      c.C = m->x; c.ldc = Cst; c.M = rows; c.N = Cst;
       c.stats_in = m->sm; c.stats_out = m->sx; c.ln_width = 4 * pv.C; c.slot_width = C;
-      EVT_RC(dense(m, st.merge, c, s));
+      bool fused = false;
+      if (dt == DT_BF16 && pv.Cst == pv.C && pv.R % 2 == 0) {
+        // the gather inside the reduction GEMM's A loader (gemm.hip, EPI_GATHER): A = the old
+        // stream, read in place, so the new stream goes to xm and the two buffers swap roles
+        DenseCall g = c;
+        g.flags |= EPI_GATHER;
+        g.A = m->x; g.lda = pv.Cst; g.C = m->xm;
+        GemmParams p = dense_params(m, st.merge, g);
+        const int R2 = pv.R / 2;
+        p.gR = pv.R; p.gC = pv.C;
+        p.g_inv_rr = 1.0f / (float)(R2 * R2); p.g_inv_r = 1.0f / (float)R2;
+        EVT_HIP(merge_stats_launch(m->sx, stats_slots(pv.C), B, pv.R, m->sm, stats_slots(C), s),
+                "merge statistics");
+        const hipError_t e = gemm_launch(dt, g.flags, p, s);
+        if (e == hipSuccess) {
+          c.A = m->x; c.lda = 4 * pv.C;  // (work accounting: the same A bytes, gathered)
+          dense_work(m, st.merge, c);
+          std::swap(m->x, m->xm);
+          fused = true;
+        } else if (e != hipErrorNotSupported) {
+          EVT_HIP(e, "patch merge (gathered)");
+        }
+      }
+      if (!fused) {
+        prof_work(m, 0.0, 2.0 * rows * 4 * pv.C * es + (double)rows * stats_slots(C) * 8);
+        EVT_HIP(merge_launch(dt, m->x, pv.Cst, B, pv.R, pv.C, m->hbuf, m->sm, stats_slots(C), s),
+                "patch merge");
+        c.A = m->hbuf; c.lda = 4 * pv.C;
+        EVT_RC(dense(m, st.merge, c, s));
+      }
     }
     for (const SwinBlock& bl : st.blocks) {
       const bool fuse96 = dt == DT_BF16 && C == 96 && st.H == 3 && gemm_variant() == 0;

@@ -20,6 +20,7 @@ enum : int {
   EPI_STATS = 128,   // accumulate (sum, sum of squares) of each output row into stats_out
   EPI_GELU_ERF = 256,  // exact erf GELU (nn.GELU, the Swin MLP)
   EPI_OUT_MX8 = 512,   // MXFP8 output (mx8.hip GEMM only)
+  EPI_GATHER = 1024,   // A rows gathered by the GEMM's loader (GemmParams gR / gC: PatchMerging)
 };
 
 // C[M, N] = epilogue(A[M, K] . W[K, N]) with W pre-packed K-contiguous as Wp[Npad][Kpad].
@@ -46,6 +47,9 @@ struct GemmParams {
   float eps;                          // LayerNorm epsilon (1e-5)
   int nslots;                         // stats rows are [nslots][2]: per-128-column-slab partials
   int stats_step;                     // EPI_LNIN: A row m reads stats_in row m * stats_step (0 = 1)
+  int gR, gC;                         // EPI_GATHER (Swin PatchMerging): A row (b, y, x) of the
+  float g_inv_rr, g_inv_r;            //   R/2 grid = the 4 source tokens' C channels of the R-grid
+                                      //   stream A (ld lda); 1/(R/2)^2, 1/(R/2)
   int* sk_flags;                      // stream-K hand-off flags [>= #CUs] (zero between launches)
   float* sk_part;                     // stream-K partial tiles [#CUs][256 * 256] fp32
   int ks_chunk;                       // split-K (128x128 kernel, gridDim.y splits): K per split;
@@ -221,6 +225,9 @@ struct SwinAttnBlockParams {
   float eps;
 };
 hipError_t swin_attn96_launch(const SwinAttnBlockParams& p, hipStream_t s);
+// statistics of gathered PatchMerging rows from the source stream's slot statistics (swin.hip)
+hipError_t merge_stats_launch(const float* src, int ns, int B, int R, float* dst, int nd,
+                              hipStream_t s);
 // fused Swin stem (swin.hip): Conv2d(3, 96, k = s = 4) + LayerNorm(96) -> bf16 stream + stats
 struct SwinEmbedParams {
   const float* img;        // [B][3][S][S] fp32 NCHW

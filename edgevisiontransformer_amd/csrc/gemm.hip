@@ -572,9 +572,31 @@ __device__ __forceinline__ void big8_bar() {
   asm volatile("" ::: "memory");
 }
 
+// Params type of the EPI_GATHER instantiations: the A loader gathers (the type selects the
+// loader at compile time; every other GEMM keeps the plain one).
+struct GatherParams : GemmParams {};
+
+// EPI_GATHER A address (Swin PatchMerging, reference SwinTransformer PatchMerging.forward:
+// x0 | x1 | x2 | x3 = x[0::2, 0::2] | x[1::2, 0::2] | x[0::2, 1::2] | x[1::2, 1::2]): GEMM row gm
+// is token (b, y, x) of the R/2 grid, element k = q C + c is channel c of source token
+// (2y + (q & 1), 2x + (q >> 1)) of the R-grid stream. Divisions by float reciprocals (exact for
+// gm < 2^22 with the half-unit offset, as pos_img).
+__device__ __forceinline__ const char* gather_addr(const GemmParams& p, int gm, int k) {
+  const int R2 = p.gR >> 1;
+  const int b = (int)(((float)gm + 0.5f) * p.g_inv_rr);
+  const int r = gm - b * R2 * R2;
+  const int y = (int)(((float)r + 0.5f) * p.g_inv_r);
+  const int x = r - y * R2;
+  const int q = (k >= p.gC) + (k >= 2 * p.gC) + (k >= 3 * p.gC);
+  const int c = k - q * p.gC;
+  const int64_t src = ((int64_t)b * p.gR + 2 * y + (q & 1)) * p.gR + 2 * x + (q >> 1);
+  return (const char*)p.A + (src * p.lda + c) * 2;
+}
+
 // DMA region j of K-tile T into buffer (T ^ par) & 1 (par: the buffer parity of the tile's
 // K-tile 0; persistent kernel with an odd K-tile count: alternates from tile to tile).
-__device__ __forceinline__ void big8_stage(const GemmParams& p, char* smem, int wave, int lane,
+template <typename P>
+__device__ __forceinline__ void big8_stage(const P& p, char* smem, int wave, int lane,
                                            int m0, int n0, int T, int j, int par = 0) {
   const int srow = lane >> 3, sslot = lane & 7;
   EVT_LDS char* base = (EVT_LDS char*)smem + ((T ^ par) & 1) * BIG_STAGE;
@@ -585,7 +607,10 @@ __device__ __forceinline__ void big8_stage(const GemmParams& p, char* smem, int 
     if (j == 0 || j == 3) {
       const int row = (r & 63) + ((r >> 6) << 7) + (j == 3 ? 64 : 0);
       const int gm = min(m0 + row + srow, p.M - 1);
-      glds16((const char*)p.A + (int64_t)gm * (p.lda * 2) + koff, base + row * ROWB);
+      if constexpr (std::is_same<P, GatherParams>::value)
+        glds16(gather_addr(p, gm, T * 64 + ((sslot ^ srow) << 3)), base + row * ROWB);
+      else
+        glds16((const char*)p.A + (int64_t)gm * (p.lda * 2) + koff, base + row * ROWB);
     } else {
       const int row = ((r >> 5) << 6) + (r & 31) + (j == 2 ? 32 : 0);
       glds16((const char*)p.W + (int64_t)(n0 + row + srow) * (p.ldw * 2) + koff,
@@ -596,7 +621,8 @@ __device__ __forceinline__ void big8_stage(const GemmParams& p, char* smem, int 
 
 __device__ __forceinline__ int big8_npro(int nk) { return min(6, 4 * nk); }
 
-__device__ __forceinline__ void big8_prologue(const GemmParams& p, char* smem, int wave, int lane,
+template <typename P>
+__device__ __forceinline__ void big8_prologue(const P& p, char* smem, int wave, int lane,
                                               int m0, int n0, int nk, int par = 0) {
   // regions s = 0..5 (tile 0, then regions 0 / 1 of tile 1); only 0..3 when nk == 1
 #pragma unroll
@@ -617,8 +643,9 @@ __device__ __forceinline__ void big8_prologue(const GemmParams& p, char* smem, i
 // final MFMA phase and group 0 the resync barrier after the loop, so group 0 starts its epilogue
 // while group 1 still issues its last 16 MFMAs (the two barriers cancel in every wave's count).
 // ph3: issues X3 further VMEM loads at the start of phase 3 (added to that phase's wait).
-template <int MODE, int X, bool OPEN = false, int X3 = 0, typename Ph3 = NoOp>
-__device__ __forceinline__ void big8_ktile(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
+template <int MODE, int X, bool OPEN = false, int X3 = 0, typename Ph3 = NoOp,
+          typename P = GemmParams>
+__device__ __forceinline__ void big8_ktile(const P& p, char* smem, f32x4 (&acc)[4][8],
                                            int wave, int lane, int wm, int wn, int m0, int n0,
                                            int t, bool cont = false, int nm0 = 0, int nn0 = 0,
                                            Ph3 ph3 = {}, int par = 0, int npar = 0) {
@@ -700,8 +727,8 @@ __device__ __forceinline__ void big8_ktile(const GemmParams& p, char* smem, f32x
 // last: issues LX further VMEM loads per wave just before the last K-tile (added to its waits:
 // they are younger than every DMA that tile waits for).
 template <int X, bool OPEN = false, typename Pre1 = NoOp, typename Mid = NoOp, int LX = 0,
-          typename Last = NoOp, int LX3 = 0, typename Last3 = NoOp>
-__device__ __forceinline__ void big8_loop(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
+          typename Last = NoOp, int LX3 = 0, typename Last3 = NoOp, typename P = GemmParams>
+__device__ __forceinline__ void big8_loop(const P& p, char* smem, f32x4 (&acc)[4][8],
                                           int wave, int lane, int wm, int wn, int m0, int n0,
                                           int nk, bool cont = false, int nm0 = 0, int nn0 = 0,
                                           Pre1 pre1 = {}, Mid mid = {}, Last last = {},
@@ -1523,8 +1550,8 @@ __device__ __forceinline__ void chain_wait(ChainCtx& cx, int tm, char* smem) {
 // ROLE 0: a plain launch; 1: chain producer (outputs write-through, each tile's panel published
 // one tile later, when every wave's stores of it have provably completed, the last one after a
 // drain); 2: chain consumer (each tile's prologue waits for its panel).
-template <int FL, int DBG, bool PADN, int ROLE>
-__device__ __forceinline__ void pers_run(const GemmParams& p, int total, int tile, char* smem,
+template <int FL, int DBG, bool PADN, int ROLE, typename P = GemmParams>
+__device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* smem,
                                          ChainCtx& cx) {
   // a quarter of the residual before the last K-tile (out-proj 160 -> 153 us); DBG 20: A/B without
   constexpr int ER = ((FL & EPI_RESID) != 0 && DBG != 7 && DBG != 20 && DBG != 18)
@@ -1663,7 +1690,13 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
   const int tile = (G & 7) ? (int)blockIdx.x : (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
   if (tile >= total) return;
   ChainCtx cx;
-  pers_run<FL, DBG, PADN, 0>(p, total, tile, smem, cx);
+  if constexpr ((FL & EPI_GATHER) != 0) {
+    GatherParams q;
+    static_cast<GemmParams&>(q) = p;
+    pers_run<FL, DBG, PADN, 0>(q, total, tile, smem, cx);
+  } else {
+    pers_run<FL, DBG, PADN, 0>(p, total, tile, smem, cx);
+  }
 }
 
 // Two dependent GEMMs in one persistent launch: producer FA (out-proj: LN residual, row
@@ -1892,7 +1925,8 @@ constexpr bool pers_fl(int fl) {
          fl == (EPI_LNIN | EPI_BIAS | EPI_GELU) ||
          fl == (EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS) ||
          fl == (EPI_LNIN | EPI_BIAS | EPI_GELU_ERF) || fl == (EPI_BIAS | EPI_RESID | EPI_STATS) ||
-         fl == (EPI_LNIN | EPI_BIAS | EPI_STATS);
+         fl == (EPI_LNIN | EPI_BIAS | EPI_STATS) ||
+         fl == (EPI_LNIN | EPI_BIAS | EPI_STATS | EPI_GATHER);
 }
 
 // persistent kernel: supported epilogue, 8-column output groups, LN rows of <= 8 slots
@@ -2005,17 +2039,26 @@ hipError_t launch_sk(const GemmParams& p, hipStream_t s) {
 
 template <typename T, int FL>
 hipError_t launch_t(const GemmParams& p, hipStream_t s) {
-  if constexpr (std::is_same<T, bf16>::value) {
-    if (use_big(p, FL)) {
-      if constexpr (pers_fl(FL)) {
-        if (use_pers(p, FL)) return use_sk(p) ? launch_sk<FL>(p, s) : launch_pers<FL>(p, s);
-      }
-      return launch_big<FL>(p, s);
+  if constexpr ((FL & EPI_GATHER) != 0) {  // the gathering loader is the persistent kernel's
+    if constexpr (std::is_same<T, bf16>::value) {
+      if (p.gR > 0 && p.gR % 2 == 0 && p.gC % 8 == 0 && p.K == 4 * p.gC && use_big(p, FL) &&
+          use_pers(p, FL) && !use_sk(p))
+        return launch_pers<FL>(p, s);
     }
+    return hipErrorNotSupported;
+  } else {
+    if constexpr (std::is_same<T, bf16>::value) {
+      if (use_big(p, FL)) {
+        if constexpr (pers_fl(FL)) {
+          if (use_pers(p, FL)) return use_sk(p) ? launch_sk<FL>(p, s) : launch_pers<FL>(p, s);
+        }
+        return launch_big<FL>(p, s);
+      }
+    }
+    const int mtiles = (p.M + GEMM_BM - 1) / GEMM_BM;
+    hipLaunchKernelGGL((gemm_nt_kernel<T, FL>), dim3(mtiles * p.ntiles), dim3(256), 0, s, p);
+    return hipGetLastError();
   }
-  const int mtiles = (p.M + GEMM_BM - 1) / GEMM_BM;
-  hipLaunchKernelGGL((gemm_nt_kernel<T, FL>), dim3(mtiles * p.ntiles), dim3(256), 0, s, p);
-  return hipGetLastError();
 }
 
 template <typename T>
@@ -2035,6 +2078,7 @@ hipError_t dispatch(int flags, const GemmParams& p, hipStream_t s) {
     EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_OUT_F32)              // LN-folded classifier (T2T)
     EVT_CASE(EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS)   // out-proj / FC2 + LN residual
     EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_GELU_ERF)             // Swin LN2-folded FC1 + erf GELU
+    EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_STATS | EPI_GATHER)   // Swin PatchMerging (gathered A)
     EVT_CASE(EPI_BIAS | EPI_RESID | EPI_STATS)               // Swin proj / FC2 + plain residual
     EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_STATS)                // Swin LN-folded patch-merge reduction
 #undef EVT_CASE

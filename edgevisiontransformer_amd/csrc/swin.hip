@@ -190,6 +190,32 @@ __global__ __launch_bounds__(256) void merge_kernel(const T* __restrict__ x, int
   }
 }
 
+// ---- statistics of the gathered PatchMerging rows (for the EPI_GATHER reduction GEMM) ----------
+// Row (b, y, x) of the R/2 grid is the concatenation of 4 source tokens, so its (sum, sumsq) is the
+// sum of their slot statistics (written by the previous stage's last sublayer): slot 0, the other
+// slots zero.
+__global__ __launch_bounds__(256) void merge_stats_kernel(const float* __restrict__ src, int ns,
+                                                          int B, int R, float* __restrict__ dst,
+                                                          int nd) {
+  const int R2 = R / 2;
+  const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (m >= (int64_t)B * R2 * R2) return;
+  const int b = (int)(m / (R2 * R2)), r = (int)(m - (int64_t)b * R2 * R2), y = r / R2, x = r - y * R2;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t row = ((int64_t)b * R + 2 * y + (q & 1)) * R + 2 * x + (q >> 1);
+    for (int j = 0; j < ns; ++j) {
+      const f32x2 v = *(const f32x2*)(src + (row * ns + j) * 2);
+      s1 += v[0];
+      s2 += v[1];
+    }
+  }
+  float* d = dst + m * nd * 2;
+  *(f32x2*)d = f32x2{s1, s2};
+  for (int j = 1; j < nd; ++j) *(f32x2*)(d + 2 * j) = f32x2{0.f, 0.f};
+}
+
 // ---- relative position bias + shift mask, expanded once per block at model creation ----------
 // dense[type][h][q][k] = table[(qy-ky+w-1)*(2w-1) + (qx-kx+w-1)][h] * log2(e), -100 * log2(e) more
 // where q and k lie in different SW-MSA regions, -inf for k >= w*w. With a shift the windows of
@@ -1163,6 +1189,16 @@ hipError_t swin_embed96_launch(const SwinEmbedParams& p, hipStream_t s) {
   const size_t lds = (size_t)96 * EMB96_WROW + 12 * p.S * 4 + 64 * EMB96_XROW;
   const int rows = p.B * (p.S / 4);
   hipLaunchKernelGGL(swin_embed96_kernel, dim3(std::min(rows, 4 * ncu)), dim3(256), lds, s, p);
+  return hipGetLastError();
+}
+
+hipError_t merge_stats_launch(const float* src, int ns, int B, int R, float* dst, int nd,
+                              hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  if (R % 2 || ns < 1 || nd < 1) return hipErrorInvalidValue;
+  const int64_t rows = (int64_t)B * (R / 2) * (R / 2);
+  hipLaunchKernelGGL(merge_stats_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, src,
+                     ns, B, R, dst, nd);
   return hipGetLastError();
 }
 
