@@ -131,6 +131,8 @@ struct evt_model {
   float* su = nullptr;       // unfold row statistics
   void* kqvb = nullptr;      // [B*T1, 192]
   void* pout = nullptr;      // [B*T1, 64] performer output (NHWC for the next unfold)
+  float* tstats = nullptr;   // [B*T1, 2] per-token (sum, sumsq) of pout (gathered soft split)
+  void* zrow = nullptr;      // 256 zero bytes: the soft split's padding rows (gathered loader)
   float* part = nullptr;     // performer partial sums
   // workspace (activation dtype unless noted)
   void* apatch = nullptr;    // [B*P, pd] patch matrix (aliases hbuf)
@@ -695,7 +697,7 @@ size_t t2t_workspace_bytes(const evt_t2t_desc* d, const T2TShape& ts, int B) {
   return t2t_unfold_elems(ts, B) * es + t2t_unfold_stat_floats(ts, B) * 4 + t1 * 4 * 64 * es +
          performer_part_floats(B, ts.grid[0] * ts.grid[0]) * 4 + 2 * rows * d->dim * es +
          2 * rows * stats_slots(d->dim) * 2 * 4 + rows * 4 * ts.enc.max_inner * es +
-         rows * ts.enc.max_ffn_st * es;
+         rows * ts.enc.max_ffn_st * es + t1 * 2 * 4 + 256;
 }
 
 
@@ -1030,6 +1032,9 @@ int evt_t2t_create(const evt_t2t_desc* desc, const float* const* w, int n_weight
     EVT_RC(dev_alloc(m, (void**)&m->su, t2t_unfold_stat_floats(ts, B) * sizeof(float)));
     EVT_RC(dev_alloc(m, &m->kqvb, t1 * 3 * 64 * es));
     EVT_RC(dev_alloc(m, &m->pout, t1 * 64 * es));
+    EVT_RC(dev_alloc(m, (void**)&m->tstats, t1 * 2 * sizeof(float)));
+    EVT_RC(dev_alloc(m, &m->zrow, 256));
+    EVT_HIP(hipMemsetAsync(m->zrow, 0, 256, s), "memset zero row");
     EVT_RC(dev_alloc(m, (void**)&m->part, performer_part_floats(B, ts.grid[0] * ts.grid[0]) *
                                               sizeof(float)));
     EVT_RC(alloc_encoder_ws(m, B, (size_t)B * ts.enc.T * ts.enc.max_ffn_st * es, s));
@@ -1073,23 +1078,48 @@ int evt_t2t_forward(evt_model* m, const float* img, int B, float* logits, void* 
     c.stats_in = m->su; c.ln_width = P1.din;
     EVT_RC(dense(m, P1.kqv, c, s));
   }
+  // soft_split1 gathered inside the kqv GEMM's A loader where it can (bf16, persistent GEMM): the
+  // performer then also writes per-token statistics, from which the split rows' are summed
+  const Performer& P2 = m->perf[1];
+  const bool gather1 = dt == DT_BF16 && P2.dpad == 9 * 64 && g2 == (g1 + 1) / 2 && m->zrow;
   {
     ProfScope ps(m, EVT_PROF_T2T_PERFORMER, s);
     prof_work(m, perf_flops * B * t1, (double)B * t1 * (3 * 64 + 64) * es);
-    EVT_HIP(performer_launch(dt, m->kqvb, 3 * 64, B, t1, P1.w, m->part, m->pout, 64, s),
+    EVT_HIP(performer_launch(dt, m->kqvb, 3 * 64, B, t1, P1.w, m->part, m->pout, 64, s,
+                             gather1 ? m->tstats : nullptr),
             "performer1");
   }
   // iteration 2: soft_split1 (k3 s2 p1) of the [B, S/4, S/4, 64] map -> TokenPerformer (:72-77)
-  const Performer& P2 = m->perf[1];
-  {
-    ProfScope ps(m, EVT_PROF_T2T_UNFOLD, s);
-    prof_work(m, 0.0, (double)B * t1 * 64 * es + (double)B * t2 * P2.din * es +
-                          (double)B * t2 * stats_slots(P2.din) * 8);
-    EVT_HIP(unfold_launch(dt, 0, m->pout, B, g1, g1, 64, 3, 2, 1, m->u, P2.dpad, m->su,
-                          stats_slots(P2.din), s),
-            "soft_split1");
+  bool fused1 = false;
+  if (gather1) {
+    ProfScope ps(m, EVT_PROF_T2T_KQV, s);
+    DenseCall c;
+    c.flags = EPI_LNIN | EPI_BIAS | EPI_GATHER;
+    c.A = m->pout; c.lda = 64; c.C = m->kqvb; c.ldc = 3 * 64; c.M = B * t2; c.N = 3 * 64;
+    c.stats_in = m->su; c.ln_width = P2.din;
+    GemmParams p = dense_params(m, P2.kqv, c);
+    p.gmode = 2; p.gR = g1; p.gC = 64; p.gOW = g2; p.gzero = m->zrow;
+    p.g_inv_rr = 1.0f / (float)(g2 * g2); p.g_inv_r = 1.0f / (float)g2;
+    EVT_HIP(unfold_stats_launch(m->tstats, B, g1, m->su, stats_slots(P2.din), s),
+            "soft_split1 statistics");
+    const hipError_t e = gemm_launch(dt, c.flags, p, s);
+    if (e == hipSuccess) {
+      c.flags &= ~EPI_GATHER;
+      dense_work(m, P2.kqv, c);
+      fused1 = true;
+    } else if (e != hipErrorNotSupported) {
+      EVT_HIP(e, "soft_split1 + kqv (gathered)");
+    }
   }
-  {
+  if (!fused1) {
+    {
+      ProfScope ps(m, EVT_PROF_T2T_UNFOLD, s);
+      prof_work(m, 0.0, (double)B * t1 * 64 * es + (double)B * t2 * P2.din * es +
+                            (double)B * t2 * stats_slots(P2.din) * 8);
+      EVT_HIP(unfold_launch(dt, 0, m->pout, B, g1, g1, 64, 3, 2, 1, m->u, P2.dpad, m->su,
+                            stats_slots(P2.din), s),
+              "soft_split1");
+    }
     ProfScope ps(m, EVT_PROF_T2T_KQV, s);
     DenseCall c;
     c.flags = EPI_LNIN | EPI_BIAS;
@@ -1377,7 +1407,7 @@ int evt_swin_forward(evt_model* m, const float* img, int B, float* logits, void*
         g.A = m->x; g.lda = pv.Cst; g.C = m->xm;
         GemmParams p = dense_params(m, st.merge, g);
         const int R2 = pv.R / 2;
-        p.gR = pv.R; p.gC = pv.C;
+        p.gmode = 1; p.gR = pv.R; p.gC = pv.C; p.gOW = R2;
         p.g_inv_rr = 1.0f / (float)(R2 * R2); p.g_inv_r = 1.0f / (float)R2;
         EVT_HIP(merge_stats_launch(m->sx, stats_slots(pv.C), B, pv.R, m->sm, stats_slots(C), s),
                 "merge statistics");

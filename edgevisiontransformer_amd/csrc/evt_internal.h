@@ -47,9 +47,10 @@ struct GemmParams {
   float eps;                          // LayerNorm epsilon (1e-5)
   int nslots;                         // stats rows are [nslots][2]: per-128-column-slab partials
   int stats_step;                     // EPI_LNIN: A row m reads stats_in row m * stats_step (0 = 1)
-  int gR, gC;                         // EPI_GATHER (Swin PatchMerging): A row (b, y, x) of the
-  float g_inv_rr, g_inv_r;            //   R/2 grid = the 4 source tokens' C channels of the R-grid
-                                      //   stream A (ld lda); 1/(R/2)^2, 1/(R/2)
+  int gR, gC;                         // EPI_GATHER: A row (b, y, x) of an OW x OW grid gathered
+  float g_inv_rr, g_inv_r;            //   from the R x R token grid A (ld lda, C channels);
+  int gmode, gOW;                     //   1/OW^2, 1/OW; gmode 1 Swin PatchMerging (OW = R/2),
+  const void* gzero;                  //   2 T2T soft split k3 s2 p1 (C = 64; gzero: zero row)
   int* sk_flags;                      // stream-K hand-off flags [>= #CUs] (zero between launches)
   float* sk_part;                     // stream-K partial tiles [#CUs][256 * 256] fp32
   int ks_chunk;                       // split-K (128x128 kernel, gridDim.y splits): K per split;
@@ -162,7 +163,11 @@ hipError_t unfold_launch(int dtype, int in_f32, const void* in, int B, int H, in
 size_t performer_part_floats(int B, int ntok);
 hipError_t performer_launch(int dtype, const void* kqv, int64_t ldq, int B, int ntok,
                             const PerformerWeights& w, float* part, void* out, int64_t ldo,
-                            hipStream_t s);
+                            hipStream_t s, float* tstats = nullptr);
+// soft split (k 3, s 2, p 1) row statistics of the R x R token map from the per-token statistics
+// performer_launch wrote (tstats: [B*R*R][2]) -> dst [rows][nslots][2] (t2t.hip)
+hipError_t unfold_stats_launch(const float* tstats, int B, int R, float* dst, int nslots,
+                               hipStream_t s);
 // CLS rows x[b*ntok] = cls + pos[0] (dtype) and their LayerNorm slot statistics.
 hipError_t cls_rows_launch(int dtype, void* x, int B, int ntok, int D, const float* cls,
                            const float* pos, float* stats, hipStream_t s);

@@ -572,21 +572,35 @@ __device__ __forceinline__ void big8_bar() {
   asm volatile("" ::: "memory");
 }
 
-// Params type of the EPI_GATHER instantiations: the A loader gathers (the type selects the
-// loader at compile time; every other GEMM keeps the plain one).
-struct GatherParams : GemmParams {};
+// Params types of the EPI_GATHER instantiations: the A loader gathers (the type selects the
+// loader at compile time; every other GEMM keeps the plain one). With EPI_STATS: the Swin
+// PatchMerging gather (gmode 1), without: the T2T soft split (gmode 2).
+struct MergeParams : GemmParams {};
+struct UnfoldParams : GemmParams {};
 
 // EPI_GATHER A address (Swin PatchMerging, reference SwinTransformer PatchMerging.forward:
 // x0 | x1 | x2 | x3 = x[0::2, 0::2] | x[1::2, 0::2] | x[0::2, 1::2] | x[1::2, 1::2]): GEMM row gm
 // is token (b, y, x) of the R/2 grid, element k = q C + c is channel c of source token
 // (2y + (q & 1), 2x + (q >> 1)) of the R-grid stream. Divisions by float reciprocals (exact for
 // gm < 2^22 with the half-unit offset, as pos_img).
+// gmode 2 (T2T soft_split1, tf_Unfold k 3 s 2 p 1 of the 64-channel token map, t2t_vit.py:72):
+// element k = (3 kh + kw) 64 + c is channel c of source token (2y - 1 + kh, 2x - 1 + kw), or of a
+// zero row outside the map.
+template <int MODE>
 __device__ __forceinline__ const char* gather_addr(const GemmParams& p, int gm, int k) {
-  const int R2 = p.gR >> 1;
+  const int OW = p.gOW;
   const int b = (int)(((float)gm + 0.5f) * p.g_inv_rr);
-  const int r = gm - b * R2 * R2;
+  const int r = gm - b * OW * OW;
   const int y = (int)(((float)r + 0.5f) * p.g_inv_r);
-  const int x = r - y * R2;
+  const int x = r - y * OW;
+  if constexpr (MODE == 2) {
+    const int win = k >> 6, c = k & 63;
+    const int kh = (win * 11) >> 5, kw = win - 3 * kh;  // win / 3 for win < 9
+    const int iy = 2 * y - 1 + kh, ix = 2 * x - 1 + kw;
+    if (iy < 0 || iy >= p.gR || ix < 0 || ix >= p.gR) return (const char*)p.gzero + c * 2;
+    const int64_t src = ((int64_t)b * p.gR + iy) * p.gR + ix;
+    return (const char*)p.A + (src * p.lda + c) * 2;
+  }
   const int q = (k >= p.gC) + (k >= 2 * p.gC) + (k >= 3 * p.gC);
   const int c = k - q * p.gC;
   const int64_t src = ((int64_t)b * p.gR + 2 * y + (q & 1)) * p.gR + 2 * x + (q >> 1);
@@ -607,8 +621,10 @@ __device__ __forceinline__ void big8_stage(const P& p, char* smem, int wave, int
     if (j == 0 || j == 3) {
       const int row = (r & 63) + ((r >> 6) << 7) + (j == 3 ? 64 : 0);
       const int gm = min(m0 + row + srow, p.M - 1);
-      if constexpr (std::is_same<P, GatherParams>::value)
-        glds16(gather_addr(p, gm, T * 64 + ((sslot ^ srow) << 3)), base + row * ROWB);
+      if constexpr (std::is_same<P, MergeParams>::value)
+        glds16(gather_addr<1>(p, gm, T * 64 + ((sslot ^ srow) << 3)), base + row * ROWB);
+      else if constexpr (std::is_same<P, UnfoldParams>::value)
+        glds16(gather_addr<2>(p, gm, T * 64 + ((sslot ^ srow) << 3)), base + row * ROWB);
       else
         glds16((const char*)p.A + (int64_t)gm * (p.lda * 2) + koff, base + row * ROWB);
     } else {
@@ -1690,8 +1706,12 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
   const int tile = (G & 7) ? (int)blockIdx.x : (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
   if (tile >= total) return;
   ChainCtx cx;
-  if constexpr ((FL & EPI_GATHER) != 0) {
-    GatherParams q;
+  if constexpr ((FL & EPI_GATHER) != 0 && (FL & EPI_STATS) != 0) {
+    MergeParams q;
+    static_cast<GemmParams&>(q) = p;
+    pers_run<FL, DBG, PADN, 0>(q, total, tile, smem, cx);
+  } else if constexpr ((FL & EPI_GATHER) != 0) {
+    UnfoldParams q;
     static_cast<GemmParams&>(q) = p;
     pers_run<FL, DBG, PADN, 0>(q, total, tile, smem, cx);
   } else {
@@ -1926,7 +1946,8 @@ constexpr bool pers_fl(int fl) {
          fl == (EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS) ||
          fl == (EPI_LNIN | EPI_BIAS | EPI_GELU_ERF) || fl == (EPI_BIAS | EPI_RESID | EPI_STATS) ||
          fl == (EPI_LNIN | EPI_BIAS | EPI_STATS) ||
-         fl == (EPI_LNIN | EPI_BIAS | EPI_STATS | EPI_GATHER);
+         fl == (EPI_LNIN | EPI_BIAS | EPI_STATS | EPI_GATHER) ||
+         fl == (EPI_LNIN | EPI_BIAS | EPI_GATHER);
 }
 
 // persistent kernel: supported epilogue, 8-column output groups, LN rows of <= 8 slots
@@ -2041,8 +2062,12 @@ template <typename T, int FL>
 hipError_t launch_t(const GemmParams& p, hipStream_t s) {
   if constexpr ((FL & EPI_GATHER) != 0) {  // the gathering loader is the persistent kernel's
     if constexpr (std::is_same<T, bf16>::value) {
-      if (p.gR > 0 && p.gR % 2 == 0 && p.gC % 8 == 0 && p.K == 4 * p.gC && use_big(p, FL) &&
-          use_pers(p, FL) && !use_sk(p))
+      constexpr bool MERGE = (FL & EPI_STATS) != 0;  // (the two gathers' instantiations)
+      const bool merge = MERGE && p.gmode == 1 && p.gR % 2 == 0 && p.gOW == p.gR / 2 &&
+                         p.gC % 8 == 0 && p.K == 4 * p.gC;
+      const bool unfold = !MERGE && p.gmode == 2 && p.gC == 64 && p.K == 9 * 64 && p.gzero &&
+                          p.gOW == (p.gR + 1) / 2;
+      if ((merge || unfold) && p.gR > 0 && use_big(p, FL) && use_pers(p, FL) && !use_sk(p))
         return launch_pers<FL>(p, s);
     }
     return hipErrorNotSupported;
@@ -2079,6 +2104,7 @@ hipError_t dispatch(int flags, const GemmParams& p, hipStream_t s) {
     EVT_CASE(EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS)   // out-proj / FC2 + LN residual
     EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_GELU_ERF)             // Swin LN2-folded FC1 + erf GELU
     EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_STATS | EPI_GATHER)   // Swin PatchMerging (gathered A)
+    EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_GATHER)               // T2T soft_split1 + kqv (gathered A)
     EVT_CASE(EPI_BIAS | EPI_RESID | EPI_STATS)               // Swin proj / FC2 + plain residual
     EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_STATS)                // Swin LN-folded patch-merge reduction
 #undef EVT_CASE

@@ -470,7 +470,8 @@ __global__ __launch_bounds__(256, 4) void performer_out16_kernel(const bf16* __r
                                                                 int64_t ldq, int ntok, int span,
                                                                 const float* __restrict__ part,
                                                                 PerformerWeights pw,
-                                                                bf16* __restrict__ out, int64_t ldo) {
+                                                                bf16* __restrict__ out, int64_t ldo,
+                                                                float* __restrict__ tstats) {
   extern __shared__ __attribute__((aligned(16))) char dsm16[];
   EVT_LDS bf16* Wl = (EVT_LDS bf16*)dsm16;
   EVT_LDS float* vec = (EVT_LDS float*)(dsm16 + PO_END * 2);  // ksum[64 (32 used)], bo, b1, b2, g2, be2
@@ -596,13 +597,26 @@ __global__ __launch_bounds__(256, 4) void performer_out16_kernel(const bf16* __r
 #pragma unroll
       for (int j = 0; j < 4; ++j) h1[nt][j] = gelu_tanh(acc[j]);
     }
+    float o1 = 0.f, o2 = 0.f;  // (sum, sumsq) of the token's stored output (tstats)
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {  // out = y2 + Dense(64)(h1)   (ffn.py:9, :99)
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int c = 0; c < 4; ++c) chain16<bf16>(acc, po_frag(Wt + PO_2, 64, nt, c, lane), h1[c]);
       acc += *(const EVT_LDS f32x4*)(vec + 192 + 16 * nt + g4) + y2[nt];
-      if (valid) store4(out + ((int64_t)b * ntok + t) * ldo + 16 * nt + g4, acc);
+      const bf16x4 ob = {(bf16)acc[0], (bf16)acc[1], (bf16)acc[2], (bf16)acc[3]};
+      if (valid) *(bf16x4*)(out + ((int64_t)b * ntok + t) * ldo + 16 * nt + g4) = ob;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float f = (float)ob[j];
+        o1 += f;
+        o2 += f * f;
+      }
+    }
+    if (tstats) {  // per-token statistics for the next soft split's gathered rows
+      o1 = token_sum(o1);
+      o2 = token_sum(o2);
+      if (valid && lane < 16) *(f32x2*)(tstats + 2 * ((int64_t)b * ntok + t)) = f32x2{o1, o2};
     }
   }
 }
@@ -761,7 +775,7 @@ __global__ __launch_bounds__(256) void performer_reduce_kernel(const float* __re
 template <typename T>
 hipError_t performer_t(const void* kqv, int64_t ldq, int B, int ntok, int chunk, int nchunk,
                        float* part, const PerformerWeights& w, int span, void* out, int64_t ldo,
-                       hipStream_t s) {
+                       hipStream_t s, float* tstats) {
   hipLaunchKernelGGL(performer_kv_kernel<T>, dim3(nchunk, B), dim3(256), 0, s, (const T*)kqv, ldq,
                      ntok, chunk, w.prmw, part);
   hipError_t e = hipGetLastError();
@@ -772,7 +786,8 @@ hipError_t performer_t(const void* kqv, int64_t ldq, int B, int ntok, int chunk,
                      part, nchunk, fin);
   if constexpr (std::is_same<T, bf16>::value) {
     hipLaunchKernelGGL(performer_out16_kernel, dim3((ntok + span - 1) / span, B), dim3(256),
-                       PF_OUT16_LDS, s, (const bf16*)kqv, ldq, ntok, span, fin, w, (bf16*)out, ldo);
+                       PF_OUT16_LDS, s, (const bf16*)kqv, ldq, ntok, span, fin, w, (bf16*)out, ldo,
+                       tstats);
     return hipGetLastError();
   }
   (void)hipFuncSetAttribute((const void*)performer_out_kernel<T>,
@@ -805,15 +820,53 @@ size_t performer_part_floats(int B, int ntok) {
 
 hipError_t performer_launch(int dtype, const void* kqv, int64_t ldq, int B, int ntok,
                             const PerformerWeights& w, float* part, void* out, int64_t ldo,
-                            hipStream_t s) {
+                            hipStream_t s, float* tstats) {
   if (B <= 0 || ntok <= 0) return hipSuccess;
   if (ldq < 3 * PF_HS || ldo < PF_HS || (ldq & 3) || (ldo & 3)) return hipErrorInvalidValue;
+  if (tstats && dtype != DT_BF16) return hipErrorInvalidValue;
   const int nchunk = performer_chunks(ntok);
   const int chunk = (ntok + nchunk - 1) / nchunk;
   const int span = 512;  // tokens per output workgroup
   return dtype == DT_BF16
-             ? performer_t<bf16>(kqv, ldq, B, ntok, chunk, nchunk, part, w, span, out, ldo, s)
-             : performer_t<float>(kqv, ldq, B, ntok, chunk, nchunk, part, w, span, out, ldo, s);
+             ? performer_t<bf16>(kqv, ldq, B, ntok, chunk, nchunk, part, w, span, out, ldo, s, tstats)
+             : performer_t<float>(kqv, ldq, B, ntok, chunk, nchunk, part, w, span, out, ldo, s,
+                                  nullptr);
+}
+
+// Statistics of the soft split (k 3, s 2, p 1) rows from per-token statistics: row (b, y, x) of
+// the OW x OW grid sums the (sum, sumsq) of its <= 9 source tokens (the zero padding adds
+// nothing); slot 0, the other slots zero.
+__global__ __launch_bounds__(256) void unfold_stats_kernel(const float* __restrict__ ts, int B,
+                                                           int R, int OW, float* __restrict__ dst,
+                                                           int nd) {
+  const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (m >= (int64_t)B * OW * OW) return;
+  const int b = (int)(m / (OW * OW)), r = (int)(m - (int64_t)b * OW * OW), y = r / OW, x = r - y * OW;
+  float s1 = 0.f, s2 = 0.f;
+  for (int kh = 0; kh < 3; ++kh) {
+    const int iy = 2 * y - 1 + kh;
+    if (iy < 0 || iy >= R) continue;
+    for (int kw = 0; kw < 3; ++kw) {
+      const int ix = 2 * x - 1 + kw;
+      if (ix < 0 || ix >= R) continue;
+      const f32x2 v = *(const f32x2*)(ts + 2 * (((int64_t)b * R + iy) * R + ix));
+      s1 += v[0];
+      s2 += v[1];
+    }
+  }
+  float* d = dst + m * nd * 2;
+  *(f32x2*)d = f32x2{s1, s2};
+  for (int j = 1; j < nd; ++j) *(f32x2*)(d + 2 * j) = f32x2{0.f, 0.f};
+}
+
+hipError_t unfold_stats_launch(const float* tstats, int B, int R, float* dst, int nslots,
+                               hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  const int OW = (R + 1) / 2;
+  const int64_t rows = (int64_t)B * OW * OW;
+  hipLaunchKernelGGL(unfold_stats_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s,
+                     tstats, B, R, OW, dst, nslots);
+  return hipGetLastError();
 }
 
 hipError_t cls_rows_launch(int dtype, void* x, int B, int ntok, int D, const float* cls,
