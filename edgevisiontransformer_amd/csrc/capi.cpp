@@ -1020,6 +1020,10 @@ int evt_t2t_create(const evt_t2t_desc* desc, const float* const* w, int n_weight
     EVT_RC(make_dense(m, &m->project, w[k + 0], w[k + 1], 9 * 64, D, s));  // t2t_vit.py:56,86
     EVT_RC(copy_vec(m, &m->cls, w[k + 2], D, s));
     EVT_RC(copy_vec(m, &m->pos, w[k + 3], (size_t)ts.enc.T * D, s));
+    if (desc->dtype == DT_BF16) {  // bf16 table for the persistent project GEMM (EPI_POS)
+      EVT_RC(dev_alloc(m, &m->pos_h, (size_t)ts.enc.T * D * 2));
+      EVT_HIP(to_bf16_launch(m->pos, m->pos_h, (int64_t)ts.enc.T * D, s), "pos -> bf16");
+    }
     k += 4;
     EVT_RC(build_encoder(m, w + k, s));
     k += 11 * desc->depth;
@@ -1094,7 +1098,7 @@ int evt_t2t_forward(evt_model* m, const float* img, int B, float* logits, void* 
   if (gather1) {
     ProfScope ps(m, EVT_PROF_T2T_KQV, s);
     DenseCall c;
-    c.flags = EPI_LNIN | EPI_BIAS | EPI_GATHER;
+    c.flags = EPI_LNIN | EPI_BIAS | EPI_SPLIT;
     c.A = m->pout; c.lda = 64; c.C = m->kqvb; c.ldc = 3 * 64; c.M = B * t2; c.N = 3 * 64;
     c.stats_in = m->su; c.ln_width = P2.din;
     GemmParams p = dense_params(m, P2.kqv, c);
@@ -1104,7 +1108,7 @@ int evt_t2t_forward(evt_model* m, const float* img, int B, float* logits, void* 
             "soft_split1 statistics");
     const hipError_t e = gemm_launch(dt, c.flags, p, s);
     if (e == hipSuccess) {
-      c.flags &= ~EPI_GATHER;
+      c.flags &= ~EPI_SPLIT;
       dense_work(m, P2.kqv, c);
       fused1 = true;
     } else if (e != hipErrorNotSupported) {
@@ -1134,13 +1138,37 @@ int evt_t2t_forward(evt_model* m, const float* img, int B, float* logits, void* 
             "performer2");
   }
   // soft_split2 -> project Dense(D) into token rows 1..P, + CLS row, + sinusoid pos (:81-86,121-125)
-  {
-    ProfScope ps(m, EVT_PROF_T2T_UNFOLD, s);
-    prof_work(m, 0.0, (double)B * t2 * 64 * es + (double)B * P * 9 * 64 * es);
-    EVT_HIP(unfold_launch(dt, 0, m->pout, B, g2, g2, 64, 3, 2, 1, m->u, 9 * 64, nullptr, 0, s),
-            "soft_split2");
+  // (the split gathered inside the project GEMM's A loader where it can, as soft_split1)
+  const int g3 = m->grid[2];
+  bool fused2 = false;
+  if (dt == DT_BF16 && g3 == (g2 + 1) / 2 && m->zrow && m->pos_h) {
+    ProfScope ps(m, EVT_PROF_PATCH_EMBED, s);
+    prof_work(m, 0.0, (double)B * D * es + (double)B * stats_slots(D) * 8);
+    EVT_HIP(cls_rows_launch(dt, m->x, B, T, D, m->cls, m->pos, m->sx, s), "cls rows");
+    DenseCall c;
+    c.flags = EPI_BIAS | EPI_POS | EPI_STATS | EPI_SPLIT;
+    c.A = m->pout; c.lda = 64; c.C = m->x; c.ldc = D; c.M = B * P; c.N = D;
+    c.pos = m->pos; c.ldp = D; c.P = P; c.stats_out = m->sx;
+    c.resid = m->pos_h; c.ldr = D;
+    GemmParams p = dense_params(m, m->project, c);
+    p.gmode = 2; p.gR = g2; p.gC = 64; p.gOW = g3; p.gzero = m->zrow;
+    p.g_inv_rr = 1.0f / (float)(g3 * g3); p.g_inv_r = 1.0f / (float)g3;
+    const hipError_t e = gemm_launch(dt, c.flags, p, s);
+    if (e == hipSuccess) {
+      c.flags &= ~EPI_SPLIT;
+      dense_work(m, m->project, c);
+      fused2 = true;
+    } else if (e != hipErrorNotSupported) {
+      EVT_HIP(e, "soft_split2 + project (gathered)");
+    }
   }
-  {
+  if (!fused2) {
+    {
+      ProfScope ps(m, EVT_PROF_T2T_UNFOLD, s);
+      prof_work(m, 0.0, (double)B * t2 * 64 * es + (double)B * P * 9 * 64 * es);
+      EVT_HIP(unfold_launch(dt, 0, m->pout, B, g2, g2, 64, 3, 2, 1, m->u, 9 * 64, nullptr, 0, s),
+              "soft_split2");
+    }
     ProfScope ps(m, EVT_PROF_PATCH_EMBED, s);
     prof_work(m, 0.0, (double)B * D * es + (double)B * stats_slots(D) * 8);
     EVT_HIP(cls_rows_launch(dt, m->x, B, T, D, m->cls, m->pos, m->sx, s), "cls rows");

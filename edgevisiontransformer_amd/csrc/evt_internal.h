@@ -20,7 +20,8 @@ enum : int {
   EPI_STATS = 128,   // accumulate (sum, sum of squares) of each output row into stats_out
   EPI_GELU_ERF = 256,  // exact erf GELU (nn.GELU, the Swin MLP)
   EPI_OUT_MX8 = 512,   // MXFP8 output (mx8.hip GEMM only)
-  EPI_GATHER = 1024,   // A rows gathered by the GEMM's loader (GemmParams gR / gC: PatchMerging)
+  EPI_GATHER = 1024,   // A rows gathered by the GEMM's loader: Swin PatchMerging (GemmParams g*)
+  EPI_SPLIT = 2048,    // A rows gathered by the GEMM's loader: T2T soft split k3 s2 p1 (g*)
 };
 
 // C[M, N] = epilogue(A[M, K] . W[K, N]) with W pre-packed K-contiguous as Wp[Npad][Kpad].

@@ -572,9 +572,9 @@ __device__ __forceinline__ void big8_bar() {
   asm volatile("" ::: "memory");
 }
 
-// Params types of the EPI_GATHER instantiations: the A loader gathers (the type selects the
-// loader at compile time; every other GEMM keeps the plain one). With EPI_STATS: the Swin
-// PatchMerging gather (gmode 1), without: the T2T soft split (gmode 2).
+// Params types of the EPI_GATHER / EPI_SPLIT instantiations: the A loader gathers (the type
+// selects the loader at compile time; every other GEMM keeps the plain one): Swin PatchMerging
+// (gmode 1) / the T2T soft split (gmode 2).
 struct MergeParams : GemmParams {};
 struct UnfoldParams : GemmParams {};
 
@@ -1706,11 +1706,11 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
   const int tile = (G & 7) ? (int)blockIdx.x : (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
   if (tile >= total) return;
   ChainCtx cx;
-  if constexpr ((FL & EPI_GATHER) != 0 && (FL & EPI_STATS) != 0) {
+  if constexpr ((FL & EPI_GATHER) != 0) {
     MergeParams q;
     static_cast<GemmParams&>(q) = p;
     pers_run<FL, DBG, PADN, 0>(q, total, tile, smem, cx);
-  } else if constexpr ((FL & EPI_GATHER) != 0) {
+  } else if constexpr ((FL & EPI_SPLIT) != 0) {
     UnfoldParams q;
     static_cast<GemmParams&>(q) = p;
     pers_run<FL, DBG, PADN, 0>(q, total, tile, smem, cx);
@@ -1947,7 +1947,7 @@ constexpr bool pers_fl(int fl) {
          fl == (EPI_LNIN | EPI_BIAS | EPI_GELU_ERF) || fl == (EPI_BIAS | EPI_RESID | EPI_STATS) ||
          fl == (EPI_LNIN | EPI_BIAS | EPI_STATS) ||
          fl == (EPI_LNIN | EPI_BIAS | EPI_STATS | EPI_GATHER) ||
-         fl == (EPI_LNIN | EPI_BIAS | EPI_GATHER);
+         fl == (EPI_LNIN | EPI_BIAS | EPI_SPLIT) || fl == (EPI_BIAS | EPI_POS | EPI_STATS | EPI_SPLIT);
 }
 
 // persistent kernel: supported epilogue, 8-column output groups, LN rows of <= 8 slots
@@ -2060,9 +2060,9 @@ hipError_t launch_sk(const GemmParams& p, hipStream_t s) {
 
 template <typename T, int FL>
 hipError_t launch_t(const GemmParams& p, hipStream_t s) {
-  if constexpr ((FL & EPI_GATHER) != 0) {  // the gathering loader is the persistent kernel's
+  if constexpr ((FL & (EPI_GATHER | EPI_SPLIT)) != 0) {  // gathering loader: persistent kernel
     if constexpr (std::is_same<T, bf16>::value) {
-      constexpr bool MERGE = (FL & EPI_STATS) != 0;  // (the two gathers' instantiations)
+      constexpr bool MERGE = (FL & EPI_GATHER) != 0;
       const bool merge = MERGE && p.gmode == 1 && p.gR % 2 == 0 && p.gOW == p.gR / 2 &&
                          p.gC % 8 == 0 && p.K == 4 * p.gC;
       const bool unfold = !MERGE && p.gmode == 2 && p.gC == 64 && p.K == 9 * 64 && p.gzero &&
@@ -2104,7 +2104,8 @@ hipError_t dispatch(int flags, const GemmParams& p, hipStream_t s) {
     EVT_CASE(EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS)   // out-proj / FC2 + LN residual
     EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_GELU_ERF)             // Swin LN2-folded FC1 + erf GELU
     EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_STATS | EPI_GATHER)   // Swin PatchMerging (gathered A)
-    EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_GATHER)               // T2T soft_split1 + kqv (gathered A)
+    EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_SPLIT)                // T2T soft_split1 + kqv (gathered A)
+    EVT_CASE(EPI_BIAS | EPI_POS | EPI_STATS | EPI_SPLIT)     // T2T soft_split2 + project
     EVT_CASE(EPI_BIAS | EPI_RESID | EPI_STATS)               // Swin proj / FC2 + plain residual
     EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_STATS)                // Swin LN-folded patch-merge reduction
 #undef EVT_CASE
