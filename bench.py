@@ -22,8 +22,9 @@ Extra objects on the JSON line:
   roofline      the dominant kernel (the role with the most device time; FC1 GEMM for DeiT-base,
                 M = 512*197, K = 768, N = 3072) timed INSIDE 5 real forwards after the timed region:
                 HIP events around each of its launches on the model's stream (evt_model_profile,
-                edgevisiontransformer_amd/profiling.py), so the figure agrees with a rocprofv3
-                kernel trace of the same command; achieved = its algorithmic FLOPs (or bytes, for
+                edgevisiontransformer_amd/profiling.py; profiled forwards run one role per launch,
+                i.e. out-proj and FC1 unchained), so the figure agrees with the rocprofv3 kernel
+                trace of the same command (its gemm_pers_kernel<35> launches); achieved = its algorithmic FLOPs (or bytes, for
                 an HBM-bound role) / avg launch time vs the 2.5 PF dense bf16 MFMA peak (8 TB/s
                 HBM); hbm_frac = algorithmic bytes / time / 8 TB/s for every role (per_role);
                 traffic = HBM bytes per launch from the rocprofv3 PMC pass committed in
@@ -299,7 +300,7 @@ def main():
                 "mfma_frac": round(fl / t_k / 1e12 / peak, 4),
                 "avg_launch_us": round(t_k * 1e6, 1), "launches_timed": 5 * k["launches"],
                 "timing": "HIP events around each launch of the role inside 5 forwards "
-                          "(evt_model_profile)",
+                          "(evt_model_profile; one role per launch: out-proj and FC1 unchained)",
                 "per_role": table}
         if dom == "fc1" and not t2t and not swin:
             M, K, N = B * model.cfg.tokens, model.cfg.dim, model.cfg.ffn[0]
@@ -325,7 +326,9 @@ def main():
                                    f"bs={cap} per GPU, {args.dtype}",
                        "model": args.model, "global_batch": G, "per_gpu_batch": cap,
                        "seq_len": model.cfg.res(0) ** 2 if swin else model.cfg.tokens,
-                       "parallelism": par},
+                       "parallelism": par,
+                       "fusion": "library default (chained out-proj -> FC1)" if args.fusion < 0
+                                 else args.fusion},
             "model_roofline": {"achieved_tflops": round(imgs_per_s * gflop_img / world / 1e3, 2),
                                "peak": peak, "frac": round(imgs_per_s * gflop_img / world / 1e3
                                                            / peak, 4),
