@@ -26,6 +26,7 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-re
 if LAB:
     FLAGS += ["-DEVT_GEMM_LAB"] + ([f"-DEVT_QA_DBG={os.environ['EVT_QA_DBG']}"]
                                    if os.environ.get("EVT_QA_DBG") else [])
+    FLAGS += os.environ.get("EVT_LAB_DEFS", "").split()  # e.g. -DEVT_MFMA_PRIO=0 (lab A/B)
 
 
 # MFMA results straight into VGPRs: with the default AGPR form the compiler parks the small

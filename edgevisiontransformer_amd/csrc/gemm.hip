@@ -558,6 +558,13 @@ struct NoOp {
   __device__ void operator()() const {}
 };
 
+// MFMA blocks of the 8-phase loop at raised wave priority (1) or not (0, the product setting:
+// measured round 3 in alternating same-box runs, lab build EVT_LAB_DEFS=-DEVT_MFMA_PRIO=...:
+// without s_setprio DeiT-base +0.4 % in 5 of 5 pairs, T2T-ViT-14 +0.55 %, Swin-T +0.37 %)
+#ifndef EVT_MFMA_PRIO
+#define EVT_MFMA_PRIO 0
+#endif
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -721,7 +728,9 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem, f32x4 (&acc)[
     big8_bar();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+#if EVT_MFMA_PRIO == 1
     __builtin_amdgcn_s_setprio(1);
+#endif
     const int mb = (ph >= 2) ? 4 : 0, nb = (ph == 1 || ph == 2) ? 2 : 0;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -730,7 +739,9 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem, f32x4 (&acc)[
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
           Mma<bf16>::run(nb ? bf1[nt][ks] : bf0[nt][ks], af[mt][ks], acc[nb + nt][mb + mt]);
+#if EVT_MFMA_PRIO == 1
     __builtin_amdgcn_s_setprio(0);
+#endif
     if (!(OPEN && MODE == 2 && ph == 3 && wm == 1)) big8_bar();
   }
 }
