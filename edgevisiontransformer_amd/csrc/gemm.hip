@@ -564,6 +564,12 @@ struct NoOp {
 #ifndef EVT_MFMA_PRIO
 #define EVT_MFMA_PRIO 0
 #endif
+// every fragment read of a phase waited for before its first MFMA (1), or the compiler's
+// per-operand lgkmcnt waits (0, the product setting: the first MFMAs start as their own
+// fragments land; +0.4 % DeiT-base in 3 of 3 alternating same-box pairs, round 3)
+#ifndef EVT_PHASE_LGKM0
+#define EVT_PHASE_LGKM0 0
+#endif
 
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -726,7 +732,9 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem, f32x4 (&acc)[
       }
     }
     big8_bar();
+#if EVT_PHASE_LGKM0
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
     __builtin_amdgcn_sched_barrier(0);
 #if EVT_MFMA_PRIO == 1
     __builtin_amdgcn_s_setprio(1);
