@@ -34,6 +34,9 @@ if LAB:
 # (v_accvgpr_read) before the softmax / GELU VALU work (96 copies per window-attention wave).
 PER_FILE_FLAGS = {s: ["-mllvm", "-amdgpu-mfma-vgpr-form=true"]
                   for s in ("attention.hip", "swin.hip", "t2t.hip")}
+# attention.hip: no NaN operands either (scores of finite bf16 / fp32 q, k; masked keys are -inf):
+# the softmax max runs on the raw MFMA results without a canonicalising v_max per element
+PER_FILE_FLAGS["attention.hip"] = PER_FILE_FLAGS["attention.hip"] + ["-fno-honor-nans"]
 # qkv_attn.hip: no NaN operands on the path, so fmaxf on raw MFMA results needs no canonicalising
 # v_max per element before the softmax max tree (-inf masking is unaffected)
 PER_FILE_FLAGS["qkv_attn.hip"] = ["-fno-honor-nans"]
@@ -52,6 +55,11 @@ def _mtime(p: str) -> float:
 
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(OBJ, exist_ok=True)
+    # a change of compile flags (EVT_LAB_DEFS, EVT_ARCH, ...) rebuilds every object
+    stamp = os.path.join(OBJ, "flags.txt")
+    want = repr((FLAGS, PER_FILE_FLAGS))
+    if not os.path.exists(stamp) or open(stamp).read() != want:
+        force = True
     hdr_t = max(_mtime(os.path.join(CSRC, h)) for h in HEADERS)
     jobs = []
     objs = []
@@ -77,6 +85,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
         list(ex.map(run, jobs))
     if force or jobs or _mtime(LIB) < max(_mtime(o) for o in objs):
         run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB])
+    with open(stamp, "w") as f:
+        f.write(want)
     return LIB
 
 

@@ -581,6 +581,11 @@ struct NoOp {
 #ifndef EVT_EPI_LGKM0
 #define EVT_EPI_LGKM0 0
 #endif
+// residual GEMMs (out-proj / FC2): L2 prefetch of the epilogue's residual tile at the start of
+// phase 3 of K-tile nk - 1 - EVT_RES_PF (0: none)
+#ifndef EVT_RES_PF
+#define EVT_RES_PF 0
+#endif
 
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -688,7 +693,8 @@ template <int MODE, int X, bool OPEN = false, int X3 = 0, typename Ph3 = NoOp,
 __device__ __forceinline__ void big8_ktile(const P& p, char* smem, f32x4 (&acc)[4][8],
                                            int wave, int lane, int wm, int wn, int m0, int n0,
                                            int t, bool cont = false, int nm0 = 0, int nn0 = 0,
-                                           Ph3 ph3 = {}, int par = 0, int npar = 0) {
+                                           Ph3 ph3 = {}, int par = 0, int npar = 0,
+                                           bool x3on = true) {
   const int frow = lane & 15, fsw = lane & 7, fg = lane >> 4;
   const EVT_LDS char* As = (const EVT_LDS char*)smem + ((t ^ par) & 1) * BIG_STAGE;
   const EVT_LDS char* Ws = As + BIG_TILE;
@@ -742,7 +748,10 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem, f32x4 (&acc)[
 #endif
     // retire what the next phase reads (phases 4, 1, 2 precede reading phases)
     if (ph != 2) {
-      if (MODE == 0) wait_vm<8 + X>();
+      if (MODE == 0) {
+        if (ph == 3 && X3 > 0 && x3on) wait_vm<8 + X + X3>();
+        else wait_vm<8 + X>();
+      }
       else if (cont) {  // the steady-state DMA pattern continues: steady-state waits
         if (ph == 3) wait_vm<8 + X + X3>();
         else wait_vm<8 + X>();
@@ -785,13 +794,16 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem, f32x4 (&acc)[
 // setup work that is then off the critical path); mid: after K-tile 0 (nk >= 3 only).
 // last: issues LX further VMEM loads per wave just before the last K-tile (added to its waits:
 // they are younger than every DMA that tile waits for).
+// pf: issues PFX further VMEM loads at the start of phase 3 of steady-state K-tile tpf (added to
+// that phase's wait; the following waits of the next K-tile retire one phase's DMA earlier).
 template <int X, bool OPEN = false, typename Pre1 = NoOp, typename Mid = NoOp, int LX = 0,
-          typename Last = NoOp, int LX3 = 0, typename Last3 = NoOp, typename P = GemmParams>
+          typename Last = NoOp, int LX3 = 0, typename Last3 = NoOp, typename P = GemmParams,
+          int PFX = 0, typename Pf = NoOp>
 __device__ __forceinline__ void big8_loop(const P& p, char* smem, f32x4 (&acc)[4][8],
                                           int wave, int lane, int wm, int wn, int m0, int n0,
                                           int nk, bool cont = false, int nm0 = 0, int nn0 = 0,
                                           Pre1 pre1 = {}, Mid mid = {}, Last last = {},
-                                          Last3 last3 = {}, int par = 0) {
+                                          Last3 last3 = {}, int par = 0, Pf pf = {}, int tpf = -1) {
   // K-tile t of this tile sits in buffer (t ^ par) & 1; the next tile (cont) starts at the parity
   // of stream K-tile nk
   const int npar = par ^ (nk & 1);
@@ -806,8 +818,15 @@ __device__ __forceinline__ void big8_loop(const P& p, char* smem, f32x4 (&acc)[4
     big8_ktile<0, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, false, 0, 0, {}, par);
     mid();
     int t = 1;
-    for (; t + 2 < nk; ++t)
-      big8_ktile<0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, false, 0, 0, {}, par);
+    for (; t + 2 < nk; ++t) {
+      if constexpr (PFX > 0) {
+        const bool on = t == tpf;  // wave-uniform
+        big8_ktile<0, 0, false, PFX>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, false, 0, 0,
+                                     [&]() { if (on) pf(); }, par, 0, on);
+      } else {
+        big8_ktile<0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, false, 0, 0, {}, par);
+      }
+    }
     big8_ktile<1, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, cont, nm0, nn0, {}, par, npar);
     last();
     big8_ktile<2, LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1, cont, nm0, nn0,
@@ -966,6 +985,8 @@ constexpr int PERS_COEF = PERS_COLRAW + 3072;   // LayerNorm (mu, r) per tile ro
 constexpr int PERS_COLB = PERS_COEF + 2048;     // column vectors of the tile being finished
 constexpr int PERS_PART = PERS_COLB + 3072;     // odd-wn waves' row partials [2][256] f32x2
 constexpr int PERS_LDS = PERS_PART + 4096;
+constexpr int PERS_SINK = PERS_LDS + 16;        // 256 B that the residual L2 prefetch DMAs into
+constexpr int PERS_LDS_ALL = PERS_SINK + 256;
 constexpr int PERS_X = 16;                      // output stores per wave per interior tile
 
 template <int FL>
@@ -1681,6 +1702,19 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
     auto last3 = [&]() {  // row pair 1 once the n-half-1 fragments are dead (phase 3)
       if constexpr (ER > 1) pers_resid_early<1, 2>(p, wm, wn, ln, m0, n0, rre);
     };
+    // residual tile pulled into L2 EVT_RES_PF K-tiles before the epilogue: two 4-B DMAs per lane
+    // (into a dead LDS sink) touch its 1024 128-B lines, so the epilogue's residual loads, which
+    // all 256 CUs issue at the same time, hit L2 instead of queueing at HBM
+    auto pf = [&]() {  // the rows the early residual loads (ER) do not cover: wm 128 + 64 .. 127
+      const int L = wave * 64 + ln;  // line: row r = L >> 2, 128-B segment L & 3
+      const int r = L >> 2;
+      const int gm = min(m0 + (r >> 6) * 128 + 64 + (r & 63), p.M - 1);
+      const int gn = min(n0 + (L & 3) * 64, p.N - 2);
+      __builtin_amdgcn_global_load_lds((const bf16*)p.resid + (int64_t)gm * p.ldr + gn,
+                                       (EVT_LDS char*)smem + PERS_SINK, 4, 0, 0);
+    };
+    constexpr int PFX = ((FL & EPI_RESID) != 0 && EVT_RES_PF > 0) ? 1 : 0;
+    const int tpf = PFX ? nk - 1 - EVT_RES_PF : -1;
     if (early) {
       // this tile's LayerNorm coefficients by wave group 1 while it waits for group 0's first
       // phase; the next tile's statistics rows / column vectors DMA'd after K-tile 0 (PERS_RAW is
@@ -1694,9 +1728,9 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
                           ntn * BIG_BN, pre1, mid, {}, {}, par);
       else
         big8_loop<PERS_X, true, decltype(pre1), decltype(mid), (ER > 0 ? 4 : 0), decltype(last),
-                  (ER > 1 ? 4 : 0), decltype(last3)>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont,
-                                                   ntm * BIG_BM, ntn * BIG_BN, pre1, mid, last,
-                                                   last3, par);
+                  (ER > 1 ? 4 : 0), decltype(last3), P, PFX, decltype(pf)>(
+            p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM, ntn * BIG_BN, pre1, mid,
+            last, last3, par, pf, tpf);
       stamp(1);
       if (has_next && !cont) {
         if constexpr (ROLE == 2) {
@@ -1709,8 +1743,9 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
       }
     } else {
       big8_loop<PERS_X, false, NoOp, NoOp, (ER > 0 ? 4 : 0), decltype(last), (ER > 1 ? 4 : 0),
-                decltype(last3)>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
-                                 ntn * BIG_BN, {}, {}, last, last3, par);
+                decltype(last3), P, PFX, decltype(pf)>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk,
+                                                       cont, ntm * BIG_BM, ntn * BIG_BN, {}, {},
+                                                       last, last3, par, pf, tpf);
       stamp(1);
       pers_coef<FL>(p, smem, tid);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1756,7 +1791,7 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
 
 template <int FL, int DBG = 0, bool PADN = true>
 __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int total) {
-  __shared__ __attribute__((aligned(16))) char smem[PERS_LDS];
+  __shared__ __attribute__((aligned(16))) char smem[PERS_LDS_ALL];
   const int G = gridDim.x;  // XCD-aware order when a multiple of 8
   const int tile = (G & 7) ? (int)blockIdx.x : (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
   if (tile >= total) return;
@@ -1784,7 +1819,7 @@ template <int FA, int FB>
 __global__ __launch_bounds__(512, 2) void gemm_chain_kernel(GemmParams pa, GemmParams pb,
                                                             int totalA, int totalB,
                                                             unsigned* sync) {
-  __shared__ __attribute__((aligned(16))) char smem[PERS_LDS + 16];
+  __shared__ __attribute__((aligned(16))) char smem[PERS_LDS_ALL];
   const int G = gridDim.x;  // multiple of 8, <= totalA (host)
   const int lb = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
   const int panels = (pa.M + BIG_BM - 1) / BIG_BM;
