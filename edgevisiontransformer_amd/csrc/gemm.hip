@@ -497,6 +497,10 @@ constexpr int BIG_STAGE = 2 * BIG_TILE;       // 64 KiB per K-tile
 // 16 stream-K. Lab builds (-DEVT_GEMM_LAB) add the ablation / timeline / A-B variants 10, 11, 13,
 // 15, 17-25, 106, 108 used by scripts/gemm_bench.py and scripts/probe/pers_timeline.py.
 thread_local int g_gemm_variant = 0;
+// Lab A/B: -DEVT_EPI_PACK_FIRST=0 (persistent epilogue without residual: swap fp32 rows, then pack)
+#ifndef EVT_EPI_PACK_FIRST
+#define EVT_EPI_PACK_FIRST 1
+#endif
 
 bool use_big(const GemmParams& p, int flags) {
   if ((p.ntiles * GEMM_BN) % BIG_BN) return false;
@@ -1403,10 +1407,15 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
   stamp(3);
   // 2. store layout: pair (2k, 2k+1) -> lane row wm*128 + (2k + (fg & 1))*16 + frow, columns
   //    wn*64 + nt*16 + (fg >> 1)*8 + [acc[nt][2k][0..3], acc[nt][2k+1][0..3]]
+  //    (no residual / position / statistics: the values are packed to bf16 first and the swap
+  //    moves 2 dwords per pair instead of 4; the same elements, bitwise the same stores)
+  constexpr bool PACK_FIRST = EVT_EPI_PACK_FIRST && (FL & (EPI_RESID | EPI_POS | EPI_STATS)) == 0;
+  if constexpr (!PACK_FIRST) {
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt)
+    for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) swap_rows16(acc[nt][2 * k], acc[nt][2 * k + 1]);
+      for (int k = 0; k < 4; ++k) swap_rows16(acc[nt][2 * k], acc[nt][2 * k + 1]);
+  }
   const int rl = wm * 128 + (fg & 1) * 16 + frow;  // + 32 k
   const int cl = wn * 64 + (fg >> 1) * 8;           // + 16 nt
   bool cok[4];
@@ -1452,8 +1461,22 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
     st[k] = f32x2{0.f, 0.f};
   }
   const bf16x2 one2 = {(bf16)1.0f, (bf16)1.0f};
+  if constexpr (PACK_FIRST) {
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const f32x4 x = acc[nt][2 * k], y = acc[nt][2 * k + 1];
+        const u32x2 xa = __builtin_bit_cast(u32x2, bf16x4{(bf16)x[0], (bf16)x[1], (bf16)x[2], (bf16)x[3]});
+        const u32x2 ya = __builtin_bit_cast(u32x2, bf16x4{(bf16)y[0], (bf16)y[1], (bf16)y[2], (bf16)y[3]});
+        unsigned x0 = xa[0], x1 = xa[1], y0 = ya[0], y1 = ya[1];
+        permlane16_swap(x0, y0);
+        permlane16_swap(x1, y1);
+        ov[k][nt] = u32x4{x0, x1, y0, y1};
+      }
+  }
+#pragma unroll
+  for (int nt = 0; nt < 4 && !PACK_FIRST; ++nt) {
     const int c = cl + 16 * nt;
     f32x4 g[2];
     if (FL & EPI_RESLN) {
