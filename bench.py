@@ -22,9 +22,9 @@ Extra objects on the JSON line:
   roofline      the dominant kernel (the role with the most device time; FC1 GEMM for DeiT-base,
                 M = 512*197, K = 768, N = 3072) timed INSIDE 5 real forwards after the timed region:
                 HIP events around each of its launches on the model's stream (evt_model_profile,
-                edgevisiontransformer_amd/profiling.py; profiled forwards run one role per launch,
-                i.e. out-proj and FC1 unchained), so the figure agrees with the rocprofv3 kernel
-                trace of the same command (its gemm_pers_kernel<35> launches); achieved = its algorithmic FLOPs (or bytes, for
+                edgevisiontransformer_amd/profiling.py; the same kernels the timed forwards run), so
+                the figure agrees with the rocprofv3 kernel trace of the same command (its
+                gemm_pers_kernel<35> launches); achieved = its algorithmic FLOPs (or bytes, for
                 an HBM-bound role) / avg launch time vs the 2.5 PF dense bf16 MFMA peak (8 TB/s
                 HBM); hbm_frac = algorithmic bytes / time / 8 TB/s for every role (per_role);
                 traffic = HBM bytes per launch from the rocprofv3 PMC pass committed in
@@ -75,8 +75,9 @@ def parse():
     ap.add_argument("--isolated-probe", action="store_true",
                     help="also time FC1 alone, back to back (reported as roofline.isolated_probe_us)")
     ap.add_argument("--fusion", type=int, default=-1,
-                    help="evt_model_set_fusion flags (-1 = the library default: 2 = chained GEMM "
-                         "launches; 0 = separate kernels; 1 = fused QKV + attention)")
+                    help="evt_model_set_fusion flags (-1 = the library default 0: separate "
+                         "kernels; 2 = chained out-proj -> FC1 GEMM launches; 1 = fused QKV + "
+                         "attention)")
     ap.add_argument("--probe-only", type=int, default=0, metavar="N",
                     help="only launch the FC1 probe kernel N times and exit (PMC collection)")
     ap.add_argument("--global-batch", type=int, default=0,
@@ -227,6 +228,8 @@ def main():
         B, G, cap = args.batch, world * args.batch, args.batch
     model = mod.build_named(args.model, dtype=args.dtype, seed=0, max_batch=cap)
     if args.fusion >= 0:
+        if not hasattr(model, "set_fusion"):  # the fusion switches are ViT / T2T-ViT ones
+            raise SystemExit(f"--fusion does not apply to {args.model}")
         model.set_fusion(args.fusion)
     if args.gemm_variant:
         from edgevisiontransformer_amd import _lib
@@ -300,7 +303,7 @@ def main():
                 "mfma_frac": round(fl / t_k / 1e12 / peak, 4),
                 "avg_launch_us": round(t_k * 1e6, 1), "launches_timed": 5 * k["launches"],
                 "timing": "HIP events around each launch of the role inside 5 forwards "
-                          "(evt_model_profile; one role per launch: out-proj and FC1 unchained)",
+                          "(evt_model_profile) of the kernels the timed forwards run",
                 "per_role": table}
         if dom == "fc1" and not t2t and not swin:
             M, K, N = B * model.cfg.tokens, model.cfg.dim, model.cfg.ffn[0]
@@ -327,7 +330,7 @@ def main():
                        "model": args.model, "global_batch": G, "per_gpu_batch": cap,
                        "seq_len": model.cfg.res(0) ** 2 if swin else model.cfg.tokens,
                        "parallelism": par,
-                       "fusion": "library default (chained out-proj -> FC1)" if args.fusion < 0
+                       "fusion": "library default (separate kernels)" if args.fusion < 0
                                  else args.fusion},
             "model_roofline": {"achieved_tflops": round(imgs_per_s * gflop_img / world / 1e3, 2),
                                "peak": peak, "frac": round(imgs_per_s * gflop_img / world / 1e3

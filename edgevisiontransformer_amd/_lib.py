@@ -28,7 +28,7 @@ EPI_BIAS, EPI_GELU, EPI_RESID, EPI_POS, EPI_OUT_F32 = 1, 2, 4, 8, 16
 EPI_LNIN, EPI_RESLN, EPI_STATS, EPI_GELU_ERF = 32, 64, 128, 256
 EPI_OUT_MX8 = 512
 FUSE_QKV_ATTENTION = 1  # evt_model_set_fusion flag (include/evt.h EVT_FUSE_QKV_ATTENTION)
-FUSE_GEMM_CHAIN = 2  # evt_model_set_fusion flag (EVT_FUSE_GEMM_CHAIN: out-proj -> FC1, default on)
+FUSE_GEMM_CHAIN = 2  # evt_model_set_fusion flag (EVT_FUSE_GEMM_CHAIN: out-proj -> FC1, opt-in)
 # evt_model_profile roles (include/evt.h EVT_PROF_*)
 PROF_ROLES = ("patchify", "patch_embed", "qkv", "attention", "out_proj", "fc1", "fc2", "head",
               "qkv_attention", "t2t_unfold", "t2t_kqv", "t2t_performer", "merge", "attn_sublayer",
@@ -114,6 +114,9 @@ SIGNATURES = {
     "evt_graph_launch": (_I, [_P, _P]),
     "evt_set_gemm_variant": (_I, [_I]),
     "evt_model_set_fusion": (_I, [_P, _I]),
+    "evt_model_status": (_I, [_P]),
+    "evt_model_set_chain_spin": (_I, [_P, _I64]),
+    "evt_diag_occupy": (_I, [_I, _I, _P]),
     "evt_model_profile": (_I, [_P, _I]),
     "evt_model_profile_read": (_I, [_P, _P, _P]),
     "evt_model_profile_work": (_I, [_P, _P, _P]),
@@ -197,3 +200,10 @@ def ensure_device(device_index: int) -> None:
 
 def stream_ptr(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def diag_occupy(blocks: int, usec: int, stream: int) -> None:
+    """Diagnostics (evt_diag_occupy): `blocks` workgroups holding one CU each for `usec` us on
+    `stream` (a torch stream's cuda_stream handle): another stream's load for the chained-launch
+    tests."""
+    check(load_library().evt_diag_occupy(int(blocks), int(usec), ctypes.c_void_p(stream)))

@@ -146,8 +146,9 @@ struct evt_model {
   size_t hbuf_bytes = 0;
   void* hh = nullptr;        // [B, head_st]
   void* sk = nullptr;        // stream-K scratch of the model's GEMMs (gemm_sk_bytes)
-  unsigned* chain = nullptr; // hand-off words of chained GEMM launches (gemm_chain_launch)
-  size_t chain_bytes = 0;
+  ChainWords chain;          // hand-off words of chained GEMM launches (gemm_chain_launch)
+  unsigned* status = nullptr; // host-mapped status word (chain.err is its device view): set by a
+                              // chained launch whose bounded hand-off wait gave up
   // Swin (family 2)
   evt_swin_desc sdesc{};
   std::vector<SwinStage> stages;
@@ -157,7 +158,7 @@ struct evt_model {
   hipGraph_t graph = nullptr;        // evt_graph_capture
   hipGraphExec_t graph_exec = nullptr;
   // evt_model_profile: HIP events around every launch of the last forward, by role
-  int fusion = EVT_FUSE_GEMM_CHAIN;  // evt_model_set_fusion
+  int fusion = 0;                    // evt_model_set_fusion
   bool prof = false;
   std::vector<hipEvent_t> prof_ev;   // pool (pairs)
   std::vector<int> prof_role;        // role of pair i of the last forward
@@ -429,10 +430,9 @@ int dense(const evt_model* m, const DenseW& w, const DenseCall& c, hipStream_t s
 // persistent launch where it qualifies (gemm_chain_launch), else the two launches.
 int dense_pair(const evt_model* m, const DenseW& wa, const DenseCall& ca, const DenseW& wb,
                const DenseCall& cb, hipStream_t s) {
-  if (!m->prof && m->chain && (m->fusion & EVT_FUSE_GEMM_CHAIN)) {
+  if (!m->prof && m->chain.sync && (m->fusion & EVT_FUSE_GEMM_CHAIN)) {
     const GemmParams pa = dense_params(m, wa, ca), pb = dense_params(m, wb, cb);
-    const hipError_t e =
-        gemm_chain_launch(m->dtype, ca.flags, pa, cb.flags, pb, m->chain, m->chain_bytes, s);
+    const hipError_t e = gemm_chain_launch(m->dtype, ca.flags, pa, cb.flags, pb, m->chain, s);
     if (e == hipSuccess) return EVT_OK;
     if (e != hipErrorNotSupported) EVT_HIP(e, "chained dense");
   }
@@ -480,6 +480,30 @@ int build_encoder(evt_model* m, const float* const* w, hipStream_t s) {
   return EVT_OK;
 }
 
+// The handle's host-mapped status word (written by kernels with system scope, read by the host
+// after the stream has synchronised: evt_model_status).
+int alloc_status(evt_model* m) {
+  if (m->status) return EVT_OK;
+  void* h = nullptr;
+  EVT_HIP(hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc status");
+  m->status = (unsigned*)h;
+  *m->status = 0;
+  void* d = nullptr;
+  EVT_HIP(hipHostGetDevicePointer(&d, h, 0), "hipHostGetDevicePointer status");
+  m->chain.err = (unsigned*)d;
+  return EVT_OK;
+}
+
+// A failure recorded by an earlier (completed) forward of the handle: EVT_EHIP once, then clear.
+int take_status(evt_model* m) {
+  if (m && m->status && __atomic_load_n(m->status, __ATOMIC_ACQUIRE) != 0) {
+    __atomic_store_n(m->status, 0u, __ATOMIC_RELEASE);
+    return fail(EVT_EHIP, "a chained GEMM hand-off wait timed out in an earlier forward of this "
+                          "handle: its logits are invalid");
+  }
+  return EVT_OK;
+}
+
 // Token-stream workspace of the encoder for B images (hbuf_bytes: the FFN hidden buffer), and the
 // stream-K scratch of the model's GEMMs (its flag block zeroed once; kernels leave it zeroed).
 int alloc_encoder_ws(evt_model* m, int B, size_t hbuf_bytes, hipStream_t s) {
@@ -498,9 +522,10 @@ int alloc_encoder_ws(evt_model* m, int B, size_t hbuf_bytes, hipStream_t s) {
   EVT_RC(dev_alloc(m, &m->o, rows * m->sh.max_inner * es));
   EVT_RC(dev_alloc(m, &m->hbuf, hbuf_bytes));
   m->hbuf_bytes = hbuf_bytes;
-  m->chain_bytes = ((rows + 255) / 256 + 3) * 4 + 16;
-  EVT_RC(dev_alloc(m, (void**)&m->chain, m->chain_bytes));
-  EVT_HIP(hipMemsetAsync(m->chain, 0, m->chain_bytes, s), "memset chain words");
+  m->chain.sync_bytes = ((rows + 255) / 256 + 3) * 4 + 16;
+  EVT_RC(dev_alloc(m, (void**)&m->chain.sync, m->chain.sync_bytes));
+  EVT_HIP(hipMemsetAsync(m->chain.sync, 0, m->chain.sync_bytes, s), "memset chain words");
+  EVT_RC(alloc_status(m));
   return EVT_OK;
 }
 
@@ -524,7 +549,7 @@ int dense_head(const evt_model* m, const DenseW& w, const DenseCall& c, hipStrea
 
 // Encoder layers (transformer_encoder.py:13-18 / :26-34) on the token stream m->x (+ stats sx).
 // Out-proj -> FC1 run as one chained launch where it qualifies (dense_pair; EVT_FUSE_GEMM_CHAIN,
-// on by default).
+// opt-in).
 int run_encoder(evt_model* m, int B, hipStream_t s) {
   const int D = m->D, T = m->sh.T, rows = B * T;
   const float log2e = 1.4426950408889634f;
@@ -818,6 +843,7 @@ int evt_model_destroy(evt_model* m) {
   if (m->graph) (void)hipGraphDestroy(m->graph);
   for (hipEvent_t e : m->prof_ev) (void)hipEventDestroy(e);
   for (void* p : m->allocs) (void)hipFree(p);
+  if (m->status) (void)hipHostFree(m->status);
   delete m;
   return EVT_OK;
 }
@@ -912,6 +938,7 @@ int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* 
   if (m->family != 0) return fail(EVT_EINVAL, "model is not a ViT (use evt_t2t_forward)");
   if (B <= 0 || B > m->max_batch)
     return fail(EVT_EINVAL, "batch must be in [1, max_batch=" + std::to_string(m->max_batch) + "]");
+  EVT_RC(take_status(m));
   hipStream_t s = (hipStream_t)stream;
   const evt_vit_desc& d = m->desc;
   const Shape& sh = m->sh;
@@ -1263,8 +1290,14 @@ int evt_graph_capture(evt_model* m, const float* img, int batch, float* logits, 
 
 int evt_graph_launch(evt_model* m, void* stream) {
   if (!m || !m->graph_exec) return fail(EVT_EINVAL, "no captured graph (call evt_graph_capture)");
+  EVT_RC(take_status(m));
   EVT_HIP(hipGraphLaunch(m->graph_exec, (hipStream_t)stream), "graph launch");
   return EVT_OK;
+}
+
+int evt_model_status(evt_model* m) {
+  if (!m) return fail(EVT_EINVAL, "model is NULL");
+  return take_status(m);
 }
 
 // ---- Swin Transformer -------------------------------------------------------------------
@@ -1576,6 +1609,20 @@ int evt_model_set_fusion(evt_model* m, int flags) {
   if (flags & ~(EVT_FUSE_QKV_ATTENTION | EVT_FUSE_GEMM_CHAIN))
     return fail(EVT_EINVAL, "unknown fusion flag");
   m->fusion = flags;
+  return EVT_OK;
+}
+
+int evt_model_set_chain_spin(evt_model* m, int64_t polls) {
+  if (!m) return fail(EVT_EINVAL, "model is NULL");
+  if (polls > 0xffffffffll) return fail(EVT_EINVAL, "polls must be <= 2^32 - 1");
+  m->chain.spin = polls < 0 ? ChainWords{}.spin : (unsigned)polls;
+  return EVT_OK;
+}
+
+int evt_diag_occupy(int blocks, int usec, void* stream) {
+  if (blocks <= 0 || usec < 0 || usec > 10000000)
+    return fail(EVT_EINVAL, "blocks must be positive and usec in [0, 1e7]");
+  EVT_HIP(occupy_launch(blocks, usec, (hipStream_t)stream), "occupy");
   return EVT_OK;
 }
 

@@ -64,12 +64,22 @@ constexpr int PAD_K = 64;   // K granularity (elements) of every packed operand
 constexpr int PAD_N = 64;   // column granularity of activation buffers
 
 hipError_t gemm_launch(int dtype, int flags, const GemmParams& p, hipStream_t s);
+// Hand-off words of chained launches: sync (>= panels + 3 words, zero when allocated; every
+// launch leaves them zeroed), err (device view of a host-mapped status word: set to 1 when a
+// bounded hand-off wait gives up), spin (poll bound of one wait, ~0.1 us per poll).
+struct ChainWords {
+  unsigned* sync = nullptr;
+  size_t sync_bytes = 0;
+  unsigned* err = nullptr;
+  unsigned spin = 1u << 23;
+};
 // Producer (fa: out-proj with the LN residual and row statistics) and consumer (fb: the LN-
-// folded FC1 + GELU reading the producer's output) in one persistent launch with per-panel
-// hand-off words in sync (>= panels + 3 words, zero when allocated; every launch leaves them
-// zeroed). hipErrorNotSupported: launch them separately.
+// folded FC1 + GELU reading the producer's output) in one persistent launch, tiles dequeued in
+// walk order, per-panel hand-offs. hipErrorNotSupported: launch them separately.
 hipError_t gemm_chain_launch(int dtype, int fa, const GemmParams& pa, int fb, const GemmParams& pb,
-                             unsigned* sync, size_t sync_bytes, hipStream_t s);
+                             const ChainWords& cw, hipStream_t s);
+// Diagnostics: `blocks` workgroups holding one CU each (all of its LDS) for `usec` microseconds.
+hipError_t occupy_launch(int blocks, int usec, hipStream_t s);
 // Skinny GEMM (small M, long K: the classifier head) as S K-splits in one launch, fp32 partials
 // part[S][M][ntiles*128], then a fixed-order reduction + bias (+ GELU) into C (deterministic).
 // flags: EPI_BIAS and/or EPI_GELU and/or EPI_OUT_F32 only; K % (S * 64) == 0.

@@ -1618,41 +1618,86 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
 // Chained launches (gemm_chain_kernel): a producer GEMM's tiles, then a consumer GEMM whose M
 // panel p may start once the producer's tiles of panel p are stored. ChainCtx is the block's view
 // of the hand-off words (zeroed by the launch): cnt[p] = producer tiles of panel p published,
-// gdone = producer tiles published in all, err = a bounded wait gave up.
+// gdone = producer tiles published in all, head = the next walk index to hand out; err = the
+// handle's host-mapped status word (a bounded wait gave up: evt_model_status reports it).
+//
+// Tiles are DEQUEUED in walk order (producer tiles 0 .. totalA - 1, then the consumer's), not
+// assigned by block index: a tile is only ever waited on after some running block has claimed it,
+// and a block's claims are increasing, so the lowest unfinished tile is always the current tile of
+// a running block whose dependencies (lower walk indices) are all finished. The walk progresses
+// whatever the residency (another stream's kernel may hold CUs, blocks may start late): no
+// co-residency assumption, no cooperative launch. A block holds its current tile, the next one
+// (whose prologue its main loop prefetches) and the ticket it takes at the top of the current tile,
+// read after that tile's epilogue (no wait on the atomic anywhere in the main loop).
 struct ChainCtx {
-  unsigned* cnt = nullptr;
-  unsigned* gdone = nullptr;
-  unsigned* err = nullptr;
-  unsigned need = 0;    // producer tiles per panel
-  unsigned totalA = 0;  // producer tiles
+  int base = 0;         // walk index of the running stage's tile 0
+  int cur = 0, nxt = 0; // walk indices: the block's current tile and the one after (uniform)
+  unsigned tk = 0;      // thread 0: the ticket taken at the top of the current tile (read after
+                        // the tile's counted waits have retired it)
   bool all_ready = false;
 };
+// The launch constants of the hand-off live in LDS (read at tile boundaries only): kept out of
+// the registers of the main loop, which has none to spare.
+struct ChainConst {
+  unsigned* cnt;
+  unsigned* gdone;
+  unsigned* head;
+  unsigned* err;
+  unsigned need;    // producer tiles per panel
+  unsigned totalA;  // producer tiles
+  unsigned total;   // producer + consumer tiles (walk length)
+  unsigned spin;    // poll bound of a hand-off wait (iterations of ~0.1 us)
+};
 
-constexpr int CHAIN_WORD = PERS_LDS;  // LDS broadcast word (the kernels allocate PERS_LDS + 16)
+constexpr int CHAIN_WORD = PERS_LDS;        // LDS broadcast word (the kernels allocate PERS_LDS + 16)
+constexpr int CHAIN_TICKET = PERS_LDS + 4;  // the ticket read at the last epilogue
+constexpr int CHAIN_CONST = PERS_LDS_ALL;   // ChainConst (gemm_chain_kernel only)
+constexpr int CHAIN_LDS_ALL = CHAIN_CONST + (int)sizeof(ChainConst);
 
-// Producer: publish panel tm (one lane; every storing wave's stores of it are complete).
-__device__ __forceinline__ void chain_publish(const ChainCtx& cx, int tm) {
-  __hip_atomic_fetch_add(cx.cnt + tm, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_fetch_add(cx.gdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ const EVT_LDS ChainConst& chain_const(const char* smem) {
+  return *(const EVT_LDS ChainConst*)(smem + CHAIN_CONST);
+}
+
+// Producer: publish panel tm (one lane, behind a barrier that every storing wave reached after its
+// vmcnt(0) drain: the guide's R1 form with write-through stores).
+__device__ __forceinline__ void chain_publish(const char* smem, int tm) {
+  const EVT_LDS ChainConst& k = chain_const(smem);
+  __hip_atomic_fetch_add(k.cnt + tm, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_add(k.gdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Thread 0: dequeue the next walk index into cx.tk (while the walk lasts). The atomic is inline asm
+// so that the compiler places no wait for its result: the caller reads cx.tk only after counted
+// vmcnt waits that retire it.
+__device__ __forceinline__ void chain_take_ticket(ChainCtx& cx, const char* smem) {
+  const EVT_LDS ChainConst& k = chain_const(smem);
+  if (cx.tk < k.total) {
+    unsigned* h = k.head;
+    unsigned one = 1u, r;
+    asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(r) : "v"(h), "v"(one) : "memory");
+    cx.tk = r;
+  }
 }
 
 // Consumer: wait (all threads, block-uniform) until panel tm is published, then one agent-scope
 // acquire; once an acquire has followed the observation that every producer tile is published,
-// later tiles need neither. Bounded (~1 s): on timeout the err word is set and the block goes on.
+// later tiles need neither. Bounded (cx.spin polls): on timeout the handle's status word is set
+// (the forward is reported failed, never silently wrong) and the block goes on.
 __device__ __forceinline__ void chain_wait(ChainCtx& cx, int tm, char* smem) {
   if (cx.all_ready) return;
   if (threadIdx.x == 0) {
+    const EVT_LDS ChainConst& k = chain_const(smem);
     bool ok = false;
-    for (int i = 0; i < (1 << 23); ++i) {
-      if (__hip_atomic_load(cx.cnt + tm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= cx.need) {
+    for (unsigned i = 0; i < k.spin; ++i) {
+      if (__hip_atomic_load(k.cnt + tm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= k.need) {
         ok = true;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    if (!ok) __hip_atomic_store(cx.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned d = __hip_atomic_load(cx.gdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *(EVT_LDS int*)(smem + CHAIN_WORD) = (d >= cx.totalA) ? 1 : 0;
+    if (!ok) __hip_atomic_store(k.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned d = __hip_atomic_load(k.gdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *(EVT_LDS int*)(smem + CHAIN_WORD) = (d >= k.totalA) ? 1 : 0;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     wait_vmcnt0();
   }
@@ -1661,17 +1706,19 @@ __device__ __forceinline__ void chain_wait(ChainCtx& cx, int tm, char* smem) {
   cx.all_ready = __builtin_amdgcn_readfirstlane(*(const EVT_LDS int*)(smem + CHAIN_WORD)) != 0;
 }
 
-// The persistent tile walk of one GEMM from logical tile `tile` in steps of gridDim.x.
-// ROLE 0: a plain launch; 1: chain producer (outputs write-through, each tile's panel published
-// one tile later, when every wave's stores of it have provably completed, the last one after a
-// drain); 2: chain consumer (each tile's prologue waits for its panel).
+// The persistent tile walk of one GEMM from logical tile `tile`: in steps of gridDim.x (ROLE 0, a
+// plain launch), or the block's dequeued walk indices (chained launch, ChainCtx): ROLE bit 1 =
+// producer (outputs write-through; a tile's panel is published at the block's next epilogue,
+// after every wave's vmcnt(0) drain and a barrier, the last one after the loop's drain), bit 2 =
+// consumer (each tile's prologue waits for its panel).
 template <int FL, int DBG, bool PADN, int ROLE, typename P = GemmParams>
 __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* smem,
                                          ChainCtx& cx) {
   // a quarter of the residual before the last K-tile (out-proj 160 -> 153 us); DBG 20: A/B without
   constexpr int ER = ((FL & EPI_RESID) != 0 && DBG != 7 && DBG != 20 && DBG != 18)
                          ? (DBG == 21 ? 1 : 2) : 0;  // DBG 21: A/B with one quarter
-  constexpr bool SC1 = ROLE == 1;
+  constexpr bool SC1 = (ROLE & 1) != 0;
+  constexpr bool WAITS = (ROLE & 2) != 0;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -1682,7 +1729,7 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
     const int q = (blockIdx.x >> 3) & 3;
     for (int i = 0; i < q * nk; ++i) __builtin_amdgcn_s_sleep(20);
   }
-  if constexpr (ROLE == 2) chain_wait(cx, tm, smem);
+  if constexpr (WAITS) chain_wait(cx, tm, smem);
   pers_coop_dma<FL>(p, smem, wave, lane, tm * BIG_BM, tn * BIG_BN);
   big8_prologue(p, smem, wave, lane, tm * BIG_BM, tn * BIG_BN, nk);
   wait_vmcnt0();  // the first K-tile's waits assume PERS_X younger VMEM ops or a drain
@@ -1698,6 +1745,11 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
   while (true) {
     const int m0 = tm * BIG_BM, n0 = tn * BIG_BN;
     stamp(0);
+    if constexpr (ROLE != 0) {
+      // the ticket naming the block's tile after `next` (read after the epilogue: by then this
+      // wave's K-tile-1 waits have retired it, vmcnt counting in issue order)
+      if (tid == 0) chain_take_ticket(cx, smem);
+    }
     f32x4 acc[4][8];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1706,15 +1758,15 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
     int ln = lane;
     asm volatile("" : "+v"(ln));  // per-tile lane addresses: not hoisted out of the tile loop
     u32x4 rre[2][4];  // ER: residual row pair 0 loaded before the last K-tile
-    const int next = tile + G;
-    const bool has_next = next < total;
+    const int next = ROLE == 0 ? tile + G : cx.nxt - cx.base;
+    const bool has_next = next >= 0 && next < total;
     int ntm = 0, ntn = 0;
     if (has_next) {
       ntm = next / p.ntiles;
       ntn = next - ntm * p.ntiles;
     }
-    // ROLE 2: the next tile's operands may be fetched ahead only once every panel is known ready
-    const bool rdy = ROLE != 2 || cx.all_ready;
+    // consumer: the next tile's operands may be fetched ahead only once every panel is known ready
+    const bool rdy = !WAITS || cx.all_ready;
     // the next tile's prologue rides in the last K-tiles' idle DMA slots (big8_ktile) as K-tiles
     // nk, nk + 1 of one stream: for odd nk the next tile starts at the other buffer parity
     const bool cont = has_next && rdy && nk >= 2 && DBG != 16 && (DBG != 6 || !(nk & 1));
@@ -1756,7 +1808,7 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
             last, last3, par, pf, tpf);
       stamp(1);
       if (has_next && !cont) {
-        if constexpr (ROLE == 2) {
+        if constexpr (WAITS) {
           if (!rdy) {  // before every panel is known ready: wait, then the skipped DMAs
             chain_wait(cx, ntm, smem);
             pers_coop_dma<FL>(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN);
@@ -1774,7 +1826,7 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       big8_bar();
       if (has_next) {
-        if constexpr (ROLE == 2) {
+        if constexpr (WAITS) {
           if (!rdy) chain_wait(cx, ntm, smem);
         }
         pers_coop_dma<FL>(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN);
@@ -1784,10 +1836,12 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     stamp(2);
-    // ROLE 1: every wave passed this tile's K-tile-1 waits (vmcnt <= 8 with more than 8 younger
-    // DMAs) before the barriers wave 0 has crossed since: the previous tile's stores are complete
-    if constexpr (ROLE == 1) {
-      if (pub_tm >= 0 && tid == 0) chain_publish(cx, pub_tm);
+    // producer: every wave passed this tile's K-tile-1 waits (vmcnt <= 8 with more than 8 younger
+    // DMAs; vmcnt counts loads, stores, atomics and LDS-DMA together in issue order,
+    // MI355X_MICROARCH.md) before the barriers wave 0 has crossed since: the previous tile's
+    // write-through stores and statistics are complete
+    if constexpr ((ROLE & 1) != 0) {
+      if (pub_tm >= 0 && tid == 0) chain_publish(smem, pub_tm);
       pub_tm = tm;
     }
     const bool interior = (m0 + BIG_BM <= p.M) && (n0 + BIG_BN <= p.N);
@@ -1796,6 +1850,13 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
     else
       pers_epilogue<FL, DBG, PADN, ER, SC1>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior,
                                             iter, rre, npar);
+    if constexpr (ROLE != 0) {  // broadcast the ticket: the block's tile after `next`
+      if (tid == 0) *(EVT_LDS unsigned*)(smem + CHAIN_TICKET) = cx.tk;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      big8_bar();
+      cx.cur = cx.nxt;
+      cx.nxt = (int)__builtin_amdgcn_readfirstlane(*(const EVT_LDS unsigned*)(smem + CHAIN_TICKET));
+    }
     stamp(7);
     ++iter;
     if (!has_next) break;
@@ -1805,10 +1866,10 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
     tm = ntm;
     tn = ntn;
   }
-  if constexpr (ROLE == 1) {  // the last tile: drain every wave, then publish
+  if constexpr ((ROLE & 1) != 0) {  // the last tile: drain every wave, then publish
     wait_vmcnt0();
     big8_bar();
-    if (tid == 0) chain_publish(cx, pub_tm);
+    if (tid == 0) chain_publish(smem, pub_tm);
   }
 }
 
@@ -1836,28 +1897,45 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
 // statistics) over every M panel, then consumer FB (FC1: LN-folded A = the producer's output) in
 // the same tile walk, so the CUs the producer's last, partial tile round
 // leaves idle start consumer tiles of panels that are already done (per-panel hand-off, acquire
-// at the consumer; DESIGN.md "Chained GEMM launches"). Every block is resident (one per CU) and
-// waits only on tiles of lower walk index, so the walk always progresses; waits are bounded.
+// at the consumer; DESIGN.md "Chained GEMM launches"). Tiles are dequeued in walk order (ChainCtx):
+// progress needs no co-residency; waits are bounded and a timeout is reported through `err`.
+// sync: [panels] counters, gdone, head, fin (zero at allocation, zeroed again by the last block).
 template <int FA, int FB>
 __global__ __launch_bounds__(512, 2) void gemm_chain_kernel(GemmParams pa, GemmParams pb,
                                                             int totalA, int totalB,
-                                                            unsigned* sync) {
-  __shared__ __attribute__((aligned(16))) char smem[PERS_LDS_ALL];
-  const int G = gridDim.x;  // multiple of 8, <= totalA (host)
-  const int lb = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+                                                            unsigned* sync, unsigned* err,
+                                                            unsigned spin) {
+  __shared__ __attribute__((aligned(16))) char smem[CHAIN_LDS_ALL];
+  const int G = gridDim.x;
   const int panels = (pa.M + BIG_BM - 1) / BIG_BM;
   ChainCtx cx;
-  cx.cnt = sync;
-  cx.gdone = sync + panels;
-  cx.err = sync + panels + 1;
-  cx.need = (unsigned)pa.ntiles;
-  cx.totalA = (unsigned)totalA;
-  if (lb < totalA) pers_run<FA, 0, false, 1>(pa, totalA, lb, smem, cx);
-  int g = lb;
-  if (g < totalA) g += ((totalA - lb + G - 1) / G) * G;  // first walk index past the producer
-  if (g - totalA < totalB) pers_run<FB, 0, false, 2>(pb, totalB, g - totalA, smem, cx);
+  // the block's first two tiles (consecutive walk indices) and the launch constants
+  if (threadIdx.x == 0) {
+    EVT_LDS ChainConst& k = *(EVT_LDS ChainConst*)(smem + CHAIN_CONST);
+    k.cnt = sync;
+    k.gdone = sync + panels;
+    k.head = sync + panels + 1;
+    k.err = err;
+    k.need = (unsigned)pa.ntiles;
+    k.totalA = (unsigned)totalA;
+    k.total = (unsigned)(totalA + totalB);
+    k.spin = spin;
+    const unsigned w0 = __hip_atomic_fetch_add(sync + panels + 1, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *(EVT_LDS unsigned*)(smem + CHAIN_TICKET) = w0;
+  }
+  __syncthreads();
+  cx.cur = (int)__builtin_amdgcn_readfirstlane(*(const EVT_LDS unsigned*)(smem + CHAIN_TICKET));
+  cx.nxt = cx.cur + 1;
+  if (cx.cur < totalA) {
+    cx.base = 0;
+    pers_run<FA, 0, false, 1>(pa, totalA, cx.cur, smem, cx);
+  }
+  if (cx.cur >= totalA && cx.cur < totalA + totalB) {
+    cx.base = totalA;
+    pers_run<FB, 0, false, 2>(pb, totalB, cx.cur - totalA, smem, cx);
+  }
   // self-cleaning hand-off words: the last block to finish (every other block is past its last
-  // poll) zeroes the counters for the next chained launch; err stays set
+  // poll and dequeue) zeroes them for the next chained launch
   unsigned* fin = sync + panels + 2;
   if (threadIdx.x == 0) {
     wait_vmcnt0();
@@ -1866,7 +1944,7 @@ __global__ __launch_bounds__(512, 2) void gemm_chain_kernel(GemmParams pa, GemmP
   }
   __syncthreads();
   if (*(const EVT_LDS unsigned*)(smem + CHAIN_WORD)) {
-    for (int i = threadIdx.x; i < panels + 1; i += blockDim.x)
+    for (int i = threadIdx.x; i < panels + 2; i += blockDim.x)
       __hip_atomic_store(sync + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 0) __hip_atomic_store(fin, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -2133,19 +2211,19 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
 // Chained producer -> consumer launch (gemm_chain_kernel). hipErrorNotSupported when the pair
 // does not qualify (the caller then launches the two GEMMs separately).
 template <int FA, int FB>
-hipError_t launch_chain(const GemmParams& pa, const GemmParams& pb, unsigned* sync,
-                        size_t sync_bytes, hipStream_t s) {
+hipError_t launch_chain(const GemmParams& pa, const GemmParams& pb, const ChainWords& cw,
+                        hipStream_t s) {
   GemmParams qa = pa, qb = pb;
   qa.ntiles = (pa.ntiles * GEMM_BN) / BIG_BN;
   qb.ntiles = (pb.ntiles * GEMM_BN) / BIG_BN;
   const int panels = (pa.M + BIG_BM - 1) / BIG_BM;
   const int totalA = panels * qa.ntiles, totalB = panels * qb.ntiles;
-  const int G = num_cus() & ~7;
-  // sync: [panels] counters, gdone, err, fin; zero at allocation, left zeroed by every launch
-  if (G < 8 || totalA < G || (size_t)(panels + 3) * 4 > sync_bytes)
+  const int G = num_cus();  // one block per CU when resident; any residency is correct
+  // sync: [panels] counters, gdone, head, fin; zero at allocation, left zeroed by every launch
+  if (G < 1 || totalA < G || (size_t)(panels + 3) * 4 > cw.sync_bytes || !cw.err)
     return hipErrorNotSupported;
   hipLaunchKernelGGL((gemm_chain_kernel<FA, FB>), dim3(G), dim3(512), 0, s, qa, qb, totalA, totalB,
-                     sync);
+                     cw.sync, cw.err, cw.spin);
   return hipGetLastError();
 }
 
@@ -2156,7 +2234,9 @@ int sk_grid() { return min(num_cus(), SK_MAX_G) & ~7; }
 // stream-K: scratch bound, auto (0) or forced (16), every range of K-iterations at least one
 // tile long (each tile has at most two parts)
 bool use_sk(const GemmParams& p) {
-  if (!p.sk_flags || !p.sk_part || g_gemm_variant != 16) return false;  // TODO auto after GPU validation
+  // explicit diagnostic only: an automatic stream-K split breaks bitwise batch-position
+  // independence ("Stream-K for the 1.5-round D = 384 GEMMs")
+  if (!p.sk_flags || !p.sk_part || g_gemm_variant != 16) return false;
   const int G = sk_grid();
   const int total = ((p.M + BIG_BM - 1) / BIG_BM) * ((p.ntiles * GEMM_BN) / BIG_BN);
   return G >= 8 && total >= G;
@@ -2180,7 +2260,9 @@ hipError_t launch_t(const GemmParams& p, hipStream_t s) {
                          p.gC % 8 == 0 && p.K == 4 * p.gC;
       const bool unfold = !MERGE && p.gmode == 2 && p.gC == 64 && p.K == 9 * 64 && p.gzero &&
                           p.gOW == (p.gR + 1) / 2;
-      if ((merge || unfold) && p.gR > 0 && use_big(p, FL) && use_pers(p, FL) && !use_sk(p))
+      // the gathered loaders decode rows with float reciprocals: exact for rows < 2^22
+      if ((merge || unfold) && p.gR > 0 && p.M < (1 << 22) && use_big(p, FL) && use_pers(p, FL) &&
+          !use_sk(p))
         return launch_pers<FL>(p, s);
     }
     return hipErrorNotSupported;
@@ -2343,15 +2425,34 @@ void gemm_sk_bind(void* ws, GemmParams& p) {
 }
 
 hipError_t gemm_chain_launch(int dtype, int fa, const GemmParams& pa, int fb, const GemmParams& pb,
-                             unsigned* sync, size_t sync_bytes, hipStream_t s) {
+                             const ChainWords& cw, hipStream_t s) {
   constexpr int RES = EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS;
-  if (dtype != DT_BF16 || g_gemm_variant != 0 || fa != RES || !sync) return hipErrorNotSupported;
+  if (dtype != DT_BF16 || g_gemm_variant != 0 || fa != RES || !cw.sync) return hipErrorNotSupported;
   if (pa.M != pb.M || pa.N % BIG_BN || pb.N % BIG_BN || pa.K / 64 < 3 || pb.K / 64 < 3 ||
       !use_pers(pa, fa) || !use_pers(pb, fb))
     return hipErrorNotSupported;
   if (fb == (EPI_LNIN | EPI_BIAS | EPI_GELU))
-    return launch_chain<RES, EPI_LNIN | EPI_BIAS | EPI_GELU>(pa, pb, sync, sync_bytes, s);
+    return launch_chain<RES, EPI_LNIN | EPI_BIAS | EPI_GELU>(pa, pb, cw, s);
   return hipErrorNotSupported;
+}
+
+// Diagnostics: `blocks` workgroups that each hold a whole CU (all 160 KiB of LDS) for `usec`
+// microseconds (s_memrealtime, 100 MHz), sleeping: the uneven-load condition of the chained-launch
+// tests (another stream's kernel keeps CUs while a forward runs).
+__global__ __launch_bounds__(64) void occupy_kernel(unsigned long long ticks, int* sink) {
+  __shared__ int hold[160 * 1024 / 4];
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+  hold[threadIdx.x] = (int)threadIdx.x;
+  __syncthreads();
+  if (hold[63 - threadIdx.x] == -1) sink[0] = 1;  // never: keeps the LDS allocation
+}
+
+hipError_t occupy_launch(int blocks, int usec, hipStream_t s) {
+  if (blocks <= 0 || usec < 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(occupy_kernel, dim3(blocks), dim3(64), 0, s,
+                     (unsigned long long)usec * 100ull, (int*)nullptr);
+  return hipGetLastError();
 }
 
 hipError_t gemm_launch(int dtype, int flags, const GemmParams& p, hipStream_t s) {

@@ -14,7 +14,7 @@
 // GEMM + attention kernels at DeiT-base bs512 (515 vs 485 us per layer): this 208 x 192, K-tile
 // 32 main loop alone takes ~365 us where the 256 x 256 8-phase persistent GEMM needs 281 us for
 // the same product, and the attention phase (~110 us) is not hidden by the co-resident workgroup.
-// Opt-in through evt_set_fusion(EVT_FUSE_QKV_ATTENTION).
+// Opt-in per model handle: evt_model_set_fusion(m, EVT_FUSE_QKV_ATTENTION).
 //
 // GEMM (as gemm.hip): transposed product C^T = W . x^T on v_mfma_f32_16x16x32_bf16 (lane: token
 // row t*16 + (lane & 15), features 4 (lane >> 4) + j), both operands K-contiguous and staged by

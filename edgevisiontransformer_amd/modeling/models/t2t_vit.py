@@ -91,7 +91,7 @@ class T2T_ViT:
 
     def set_fusion(self, flags: int) -> None:
         """Fused-kernel switches of this model (evt_model_set_fusion; _lib.FUSE_QKV_ATTENTION:
-        LN1-folded QKV + attention as one kernel; _lib.FUSE_GEMM_CHAIN, the library default:
+        LN1-folded QKV + attention as one kernel; _lib.FUSE_GEMM_CHAIN:
         chained out-proj -> FC1 launches). Kept across re-plans for larger
         batches."""
         self._fusion = int(flags)

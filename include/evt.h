@@ -157,18 +157,29 @@ int evt_model_profile_read(evt_model* m, float* us, int* launches);
  * role's time for the MFMA and HBM roofline fractions. */
 int evt_model_profile_work(evt_model* m, double* gflop, double* gbytes);
 
-/* Fused-kernel switches of ONE model handle (default EVT_FUSE_GEMM_CHAIN):
+/* Fused-kernel switches of ONE model handle (default 0: none):
  * EVT_FUSE_QKV_ATTENTION runs each bf16 ViT layer's LN1-folded QKV Dense and attention core as
  * one kernel (evt_qkv_attention) where the token count allows. Opt-in: measured slower than the
  * separate kernels at DeiT-base bs512 ("Fused QKV + attention").
  * EVT_FUSE_GEMM_CHAIN runs each bf16 ViT layer's out-proj -> FC1 as one chained persistent launch
  * where the shapes allow (FC1 tiles start on the CUs the out-proj's last tile round leaves idle;
- * bitwise the same results; DESIGN.md, "Chained GEMM launches"). Not used while the handle is
- * profiling (evt_model_profile brackets one role per launch).
+ * bitwise the same results; DESIGN.md, "Chained GEMM launches"). Tiles are dequeued in dependency
+ * order, so the launch completes whatever other streams' kernels occupy; its hand-off waits are
+ * bounded, and a wait that gives up is reported by evt_model_status (never a silent result).
+ * Opt-in: with dequeued tiles it measured 0.9 % slower than the separate launches at DeiT-base
+ * bs512.
+ * Not used while the handle is profiling (evt_model_profile brackets one role per launch).
  * Takes effect at the next forward / graph capture of that handle; other handles are unaffected. */
 #define EVT_FUSE_QKV_ATTENTION 1
 #define EVT_FUSE_GEMM_CHAIN 2
 int evt_model_set_fusion(evt_model* m, int flags);
+
+/* Deferred device-side failures of the handle's forwards: EVT_EHIP (with evt_last_error) if a
+ * forward that has COMPLETED since the last call hit a failure only the device can see (a chained
+ * GEMM hand-off wait that timed out: that forward's logits are invalid), else EVT_OK; the report
+ * is consumed. Synchronise the forward's stream first to cover a given forward; evt_vit_forward
+ * and evt_graph_launch also return it (before enqueuing anything) for earlier forwards. */
+int evt_model_status(evt_model* m);
 
 /* Pack a Keras [K, N] fp32 kernel into the GEMM operand layout Wp[Npad][Kpad] (dtype), zero
  * padded, optionally scaling row k by row_scale[k] (a LayerNorm gamma folded into the weights;
@@ -450,6 +461,15 @@ int evt_attention_mx8(const void* qkv, int64_t ldq, void* q8, int64_t ldq8, uint
  * EVT_LAB=1 (-DEVT_GEMM_LAB) also accept the ablation / timeline variants 10, 11, 13, 15, 17-25,
  * 106, 108; other values return EVT_EINVAL. */
 int evt_set_gemm_variant(int variant);
+
+/* Poll bound of the handle's chained-launch hand-off waits (~0.1 us per poll; default 2^23,
+ * a negative value restores it). 0 makes every first wait of a block give up at once: the
+ * failure-reporting path of evt_model_status, for tests. */
+int evt_model_set_chain_spin(evt_model* m, int64_t polls);
+
+/* Launch `blocks` workgroups on `stream` that each hold a whole CU (all 160 KiB of its LDS) for
+ * `usec` microseconds: uneven-load conditions for the chained-launch tests. */
+int evt_diag_occupy(int blocks, int usec, void* stream);
 
 #ifdef __cplusplus
 }

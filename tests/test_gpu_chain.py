@@ -1,9 +1,14 @@
 """Chained GEMM launches (EVT_FUSE_GEMM_CHAIN, gemm.hip gemm_chain_kernel): each DeiT-base layer's
 out-proj -> FC1 in one persistent launch, FC1's M panels handed over per panel inside the launch
-(write-through stores, per-panel counters, agent-scope acquire; counters self-cleaning). The chained forward computes every tile with the same code and reduction order as the
-separate launches, so the logits must be BITWISE equal to the unchained forward (a stale read of
-a handed-off panel shows as a difference), on every one of several repeated forwards. Reference
-ops: `attention.py:35`, `ffn.py:8-9`, `residual.py:9`."""
+(write-through stores, per-panel counters, agent-scope acquire; counters self-cleaning). Tiles are
+dequeued in walk order, so the launch completes whatever occupies the other CUs; hand-off waits
+are bounded and a wait that gives up is reported (evt_model_status), never silently wrong.
+
+The chained forward computes every tile with the same code and reduction order as the separate
+launches, so the logits must be BITWISE equal to the unchained forward (a stale read of a handed-off
+panel shows as a difference), on every one of several repeated forwards, also while another
+stream's kernel holds most of the CUs. Reference ops: `attention.py:35`, `ffn.py:8-9`,
+`residual.py:9`."""
 import pytest
 import torch
 
@@ -12,8 +17,7 @@ from edgevisiontransformer_amd import _lib
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("batch", [111, 128, 512])
-def test_chain_bitwise_equals_separate_launches(gpu, batch):
+def _model_and_ref(gpu, batch):
     from edgevisiontransformer_amd.modeling.models.vit import build_named
     m = build_named("deit_base", dtype="bf16", seed=3, max_batch=batch)
     g = torch.Generator(device=gpu).manual_seed(batch)
@@ -23,6 +27,12 @@ def test_chain_bitwise_equals_separate_launches(gpu, batch):
     m.forward_into(img, ref)
     torch.cuda.synchronize()
     m.set_fusion(_lib.FUSE_GEMM_CHAIN)
+    return m, img, ref
+
+
+@pytest.mark.parametrize("batch", [111, 128, 512])
+def test_chain_bitwise_equals_separate_launches(gpu, batch):
+    m, img, ref = _model_and_ref(gpu, batch)
     out = torch.empty_like(ref)
     bad = []
     for r in range(6):
@@ -31,5 +41,58 @@ def test_chain_bitwise_equals_separate_launches(gpu, batch):
         torch.cuda.synchronize()
         if not torch.equal(out, ref):
             bad.append((r, int((out != ref).sum())))
+    m.check_status()
     assert not bad, f"chained forwards differing from the separate launches (run, elements): {bad}"
     assert torch.isfinite(ref).all()
+
+
+@pytest.mark.parametrize("busy_cus", [64, 224, 255])
+def test_chain_under_uneven_load(gpu, busy_cus):
+    """Another stream's kernel holds `busy_cus` CUs (all their LDS) for 0.3 s while chained forwards
+    run: the walk must progress on the CUs left (a static tile walk would wait on producer tiles of
+    blocks that are not resident) and the logits stay bitwise those of the separate launches."""
+    m, img, ref = _model_and_ref(gpu, 128)
+    side = torch.cuda.Stream(gpu)
+    out = torch.empty_like(ref)
+    bad = []
+    for r in range(3):
+        out.fill_(float("nan"))
+        side.wait_stream(torch.cuda.current_stream(gpu))
+        _lib.diag_occupy(busy_cus, 300000, side.cuda_stream)
+        m.forward_into(img, out)
+        torch.cuda.synchronize()
+        if not torch.equal(out, ref):
+            bad.append((r, int((out != ref).sum())))
+    m.check_status()
+    assert not bad, f"chained forwards under load differing (run, elements): {bad}"
+
+
+def test_chain_wait_timeout_is_reported(gpu):
+    """A hand-off wait that gives up (forced: poll bound 0) must surface as an error, both from
+    check_status and from the next forward call; after restoring the bound the chained forward is
+    bitwise right again."""
+    m, img, ref = _model_and_ref(gpu, 128)
+    out = torch.empty_like(ref)
+    m.set_chain_spin(0)
+    m.forward_into(img, out)
+    torch.cuda.synchronize()
+    with pytest.raises(_lib.EvtError) as ei:
+        m.check_status()
+    assert ei.value.code == _lib.EVT_EHIP and "hand-off" in str(ei.value)
+    m.check_status()  # the report is consumed
+    m.forward_into(img, out)  # fails again (bound still 0) ...
+    torch.cuda.synchronize()
+    with pytest.raises(_lib.EvtError):
+        m.forward_into(img, out)  # ... and the NEXT forward call reports it before enqueuing
+    m.set_chain_spin(-1)
+    out.fill_(float("nan"))
+    m.forward_into(img, out)
+    torch.cuda.synchronize()
+    m.check_status()
+    assert torch.equal(out, ref)
+    # the reference-style call synchronises and checks by itself
+    m.set_chain_spin(0)
+    with pytest.raises(_lib.EvtError):
+        m(img)
+    m.set_chain_spin(-1)
+    assert torch.equal(m(img), ref)
