@@ -126,6 +126,7 @@ SIGNATURES = {
     "evt_dense": (_I, [_I, ctypes.POINTER(evt_dense_args), _P]),
     "evt_dense_splitk": (_I, [_I, ctypes.POINTER(evt_dense_args), _I, _P, _P]),
     "evt_attention": (_I, [_I, _P, _I64, _P, _I64, _I, _I, _I, _F, _P]),
+    "evt_attention_hd": (_I, [_I, _P, _I64, _P, _I64, _I, _I, _I, _I, _F, _P]),
     "evt_layernorm": (_I, [_I, _P, _I64, _P, _I64, _P, _P, _I, _I, _F, _P]),
     "evt_patchify": (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P]),
     "evt_patchify_cm": (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P]),

@@ -377,6 +377,269 @@ __global__ __launch_bounds__(64 * ATTN_F32_WAVES) void attn_f32_kernel(AttnParam
   }
 }
 
+// ---- any head size (attention.py:6-12: h_k = dim // heads; attention_launch routes h_k != 64
+// here). Same transposed-product structure as the head-size-64 kernels above.
+//
+// bf16: one workgroup (4 waves) per (image, head). K and V rows are staged to LDS with the head
+// feature axis zero-padded to DP (h_k rounded up to 32, one k-step of v_mfma_f32_16x16x32_bf16),
+// rows of DP * 2 bytes, 16-B chunk c of row r at chunk c ^ (r & SWM) (SWM: 7 / 3 when the chunk
+// count is a power of two >= 8 / = 4, else unswizzled). S^T = K Q^T takes DP / 32 MFMA steps per
+// 16-key tile, O^T = V^T P^T DP / 16 output tiles with V^T from ds_read_b64_tr_b16.
+template <int DP>
+constexpr int gen_swm() {
+  constexpr int nch = DP / 8;
+  return nch == 4 ? 3 : ((nch >= 8 && (nch & (nch - 1)) == 0) ? 7 : 0);
+}
+
+// 8 consecutive head features [d0, d0 + 8) of row `row` (bf16), zero past h_k
+__device__ __forceinline__ u32x4 gen_chunk(const bf16* row, int d0, int hd) {
+  if ((hd & 7) == 0) {
+    if (d0 < hd) return *(const u32x4*)(row + d0);
+    return u32x4{0u, 0u, 0u, 0u};
+  }
+  bf16x8 v;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = d0 + e < hd ? row[d0 + e] : (bf16)0.f;
+  return __builtin_bit_cast(u32x4, v);
+}
+
+template <int NKT, int DP>
+__global__ __launch_bounds__(256) void attn_gen_bf16_kernel(AttnParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NP = NKT * 16, NCH = DP / 8, RB = DP * 2, SWM = gen_swm<DP>(), KS = DP / 32;
+  EVT_LDS char* Ks = (EVT_LDS char*)smem;
+  EVT_LDS char* Vs = Ks + NP * RB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x / p.H, h = blockIdx.x - b * p.H, hd = p.hd;
+  const bf16* qkv = (const bf16*)p.qkv + (int64_t)b * p.N * p.ldq;
+  for (int i = tid; i < NP * NCH; i += 256) {
+    const int row = i / NCH, ch = i - row * NCH;
+    const bf16* rp = qkv + (int64_t)min(row, p.N - 1) * p.ldq;
+    const int so = row * RB + ((ch ^ (row & SWM)) << 4);
+    *(EVT_LDS u32x4*)(Ks + so) = gen_chunk(rp + (p.H + h) * hd, ch * 8, hd);
+    *(EVT_LDS u32x4*)(Vs + so) = gen_chunk(rp + (2 * p.H + h) * hd, ch * 8, hd);
+  }
+  __syncthreads();
+  const int g = lane >> 4, c16 = lane & 15;
+  const int tq = (lane >> 2) & 3, tp = lane & 3;
+  const int nqt = (p.N + 15) >> 4;
+  for (int qt = wave; qt < nqt; qt += 4) {
+    const bf16* qrow = qkv + (int64_t)min(qt * 16 + c16, p.N - 1) * p.ldq + h * hd;
+    u32x4 qf[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = gen_chunk(qrow, 32 * ks + 8 * g, hd);
+    f32x4 s[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      const int row = kt * 16 + c16;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const u32x4 kf = *(const EVT_LDS u32x4*)(Ks + row * RB + (((4 * ks + g) ^ (row & SWM)) << 4));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf),
+                                                      __builtin_bit_cast(bf16x8, qf[ks]), acc, 0, 0, 0);
+      }
+      s[kt] = acc;  // S^T[key = kt*16 + 4g + j][query = qt*16 + c16]
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (kt * 16 + 4 * g + j >= p.N) s[kt][j] = -INFINITY;
+        mx = fmaxf(mx, s[kt][j]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float moff = mx * p.scale_log2;
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float e = __builtin_amdgcn_exp2f(s[kt][j] * p.scale_log2 - moff);
+        s[kt][j] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    f32x4 o[DP / 16];
+#pragma unroll
+    for (int dt = 0; dt < DP / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < (NKT + 1) / 2; ++ks) {
+      const bool half = 2 * ks + 1 >= NKT;  // odd NKT: the last 16 keys, upper k half zero
+      bf16x8 pf;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pf[j] = (bf16)s[2 * ks][j];
+        pf[4 + j] = half ? (bf16)0.f : (bf16)s[min(2 * ks + 1, NKT - 1)][j];
+      }
+      const int key0 = ks * 32 + 4 * g + tq;
+      const int ksw = key0 & SWM;
+#pragma unroll
+      for (int dt = 0; dt < DP / 16; ++dt) {
+        const int off = (((2 * dt + (tp >> 1)) ^ ksw) << 4) + (tp & 1) * 8;
+        const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((EVT_LDS i16x4*)(Vs + key0 * RB + off));
+        const i16x4 v1 = half ? i16x4{0, 0, 0, 0}
+                              : __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                                    (EVT_LDS i16x4*)(Vs + (key0 + 16) * RB + off));
+        const i16x8 vv = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[dt],
+                                                        0, 0, 0);
+      }
+    }
+    // o[dt][j] = O^T[d = dt*16 + 4g + j][query]
+    const int q = qt * 16 + c16;
+    if (q < p.N) {
+      const float inv = 1.0f / sum;
+      bf16* op = (bf16*)p.out + ((int64_t)b * p.N + q) * p.ldo + h * hd;
+#pragma unroll
+      for (int dt = 0; dt < DP / 16; ++dt) {
+        const int d0 = dt * 16 + 4 * g;
+        if ((hd & 3) == 0) {
+          if (d0 < hd) store4(op + d0, o[dt] * inv);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (d0 + j < hd) op[d0 + j] = (bf16)(o[dt][j] * inv);
+        }
+      }
+    }
+  }
+}
+
+// fp32 (the exact parity path): one workgroup (4 waves) per (image, head), every operand read
+// straight from the qkv rows (L2-resident per head): S^T = K Q^T on v_mfma_f32_16x16x4_f32 over
+// 16-feature chunks, O^T = V^T P^T with MFMA row m of output tile (grp, dt) = head feature
+// 64 grp + 4 m + dt; NG = ceil(h_k / 64) feature groups.
+__device__ __forceinline__ f32x4 gen_load4(const float* row, int d0, int hd) {
+  if ((hd & 3) == 0) return d0 < hd ? *(const f32x4*)(row + d0) : f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = d0 + e < hd ? row[d0 + e] : 0.f;
+  return v;
+}
+
+template <int NKT, int NG>
+__global__ __launch_bounds__(256) void attn_gen_f32_kernel(AttnParams p) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x / p.H, h = blockIdx.x - b * p.H, hd = p.hd;
+  const float* qkv = (const float*)p.qkv + (int64_t)b * p.N * p.ldq;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int nqt = (p.N + 15) >> 4;
+  for (int qt = wave; qt < nqt; qt += 4) {
+    const float* qrow = qkv + (int64_t)min(qt * 16 + c16, p.N - 1) * p.ldq + h * hd;
+    f32x4 s[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kk = 0; kk < 4 * NG; ++kk) {
+      const int d0 = 16 * kk + 4 * g;
+      const f32x4 qf = gen_load4(qrow, d0, hd);
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        const float* krow = qkv + (int64_t)min(kt * 16 + c16, p.N - 1) * p.ldq + (p.H + h) * hd;
+        const f32x4 kf = gen_load4(krow, d0, hd);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[e], qf[e], s[kt], 0, 0, 0);
+      }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (kt * 16 + 4 * g + j >= p.N) s[kt][j] = -INFINITY;
+        mx = fmaxf(mx, s[kt][j]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float moff = mx * p.scale_log2;
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float e = exp2f(s[kt][j] * p.scale_log2 - moff);
+        s[kt][j] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    f32x4 o[NG][4];
+#pragma unroll
+    for (int gr = 0; gr < NG; ++gr)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[gr][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int key = min(kt * 16 + 4 * g + e, p.N - 1);  // P is 0 for keys past N
+        const float* vrow = qkv + (int64_t)key * p.ldq + (2 * p.H + h) * hd;
+#pragma unroll
+        for (int gr = 0; gr < NG; ++gr) {
+          const f32x4 v = gen_load4(vrow, 64 * gr + 4 * c16, hd);
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt)
+            o[gr][dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[dt], s[kt][e], o[gr][dt], 0, 0, 0);
+        }
+      }
+    const int q = qt * 16 + c16;
+    if (q < p.N) {
+      const float inv = 1.0f / sum;
+      float* op = (float*)p.out + ((int64_t)b * p.N + q) * p.ldo + h * hd;
+      // lane holds O[d = 64 grp + 16 g + 4 j + dt][q] in o[grp][dt][j]
+#pragma unroll
+      for (int gr = 0; gr < NG; ++gr)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int d0 = 64 * gr + 16 * g + 4 * j;
+          const f32x4 v = f32x4{o[gr][0][j], o[gr][1][j], o[gr][2][j], o[gr][3][j]} * inv;
+          if ((hd & 3) == 0) {
+            if (d0 < hd) store4(op + d0, v);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (d0 + e < hd) op[d0 + e] = v[e];
+          }
+        }
+    }
+  }
+}
+
+template <int NKT, int DP>
+hipError_t launch_gen_bf16(const AttnParams& p, hipStream_t s) {
+  const size_t lds = 2 * (size_t)NKT * 16 * DP * 2;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)attn_gen_bf16_kernel<NKT, DP>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((attn_gen_bf16_kernel<NKT, DP>), dim3(p.B * p.H), dim3(256), lds, s, p);
+  return hipGetLastError();
+}
+
+template <int NKT>
+hipError_t launch_gen(int dtype, const AttnParams& p, hipStream_t s) {
+  if (dtype == DT_BF16) {
+    if (p.hd <= 32) return launch_gen_bf16<NKT, 32>(p, s);
+    if (p.hd <= 64) return launch_gen_bf16<NKT, 64>(p, s);
+    if (p.hd <= 96) return launch_gen_bf16<NKT, 96>(p, s);
+    return launch_gen_bf16<NKT, 128>(p, s);
+  }
+  if (p.hd <= 64)
+    hipLaunchKernelGGL((attn_gen_f32_kernel<NKT, 1>), dim3(p.B * p.H), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((attn_gen_f32_kernel<NKT, 2>), dim3(p.B * p.H), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t attention_gen_launch(int dtype, const AttnParams& p, hipStream_t s) {
+  if (p.N <= 64) return launch_gen<4>(dtype, p, s);
+  if (p.N <= 128) return launch_gen<8>(dtype, p, s);
+  if (p.N <= 208) return launch_gen<13>(dtype, p, s);
+  return launch_gen<16>(dtype, p, s);
+}
+
 template <int NKT>
 hipError_t launch_nkt(int dtype, const AttnParams& p, hipStream_t s) {
   const int rowb = dtype == DT_BF16 ? 128 : 256;
@@ -398,9 +661,9 @@ bool g_attr_set = false;
 void set_lds_attrs() {
   if (g_attr_set) return;
   g_attr_set = true;
-  hipFuncSetAttribute((const void*)attn_f32_kernel<14>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  (void)hipFuncSetAttribute((const void*)attn_f32_kernel<14>, hipFuncAttributeMaxDynamicSharedMemorySize,
                       2 * 14 * 16 * 256);
-  hipFuncSetAttribute((const void*)attn_f32_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  (void)hipFuncSetAttribute((const void*)attn_f32_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
                       2 * 16 * 16 * 256);
 }
 
@@ -408,7 +671,11 @@ void set_lds_attrs() {
 
 hipError_t attention_launch(int dtype, const AttnParams& p, hipStream_t s) {
   if (p.B <= 0) return hipSuccess;
-  if (p.N <= 0 || p.N > 256 || p.H <= 0) return hipErrorInvalidValue;
+  if (p.N <= 0 || p.N > 256 || p.H <= 0 || p.hd <= 0 || p.hd > 128) return hipErrorInvalidValue;
+  if (p.hd != 64) {  // any other head size: the generic kernels (MX8 output: head size 64 only)
+    if (p.q8) return hipErrorInvalidValue;
+    return attention_gen_launch(dtype, p, s);
+  }
   set_lds_attrs();
   if (p.N <= 64) return launch_nkt<4>(dtype, p, s);
   if (p.N <= 128) return launch_nkt<8>(dtype, p, s);

@@ -71,7 +71,7 @@ struct Mx8W {  // MXFP8-packed Dense layer (mx8.hip): Wq [npad][kpad] e4m3, scal
 };
 
 struct Layer {
-  int heads = 0, inner = 0, ffn = 0, ffn_st = 0;
+  int heads = 0, hd = 64, inner = 0, ffn = 0, ffn_st = 0;
   float *ln1_g = nullptr, *ln1_b = nullptr, *ln2_g = nullptr, *ln2_b = nullptr;
   DenseW qkv, out, fc1, fc2;
   Mx8W mqkv, mout, mfc1, mfc2;  // EVT_DTYPE_MX8 models
@@ -226,8 +226,10 @@ int validate(const evt_vit_desc* d, Shape* sh) {
     return fail(EVT_EINVAL, "image dimensions must be divisible by the patch size");
   if (d->in_chans <= 0 || d->num_classes <= 0 || d->depth < 0 || d->mlp_dim <= 0)
     return fail(EVT_EINVAL, "in_chans, num_classes, mlp_dim must be positive, depth >= 0");
-  if (d->dim <= 0 || d->dim % 64 != 0 || d->dim > 1024)
-    return fail(EVT_EINVAL, "dim must be a positive multiple of 64 and <= 1024");
+  if (d->dim <= 0 || d->dim % 8 != 0 || d->dim > 1024)
+    return fail(EVT_EINVAL, "dim must be a positive multiple of 8 and <= 1024");
+  if (d->dtype == EVT_DTYPE_MX8 && d->dim % 64 != 0)
+    return fail(EVT_EINVAL, "EVT_DTYPE_MX8 needs dim % 64 == 0");
   if (d->max_batch <= 0) return fail(EVT_EINVAL, "max_batch must be positive");
   if (d->semantics != EVT_VIT_REFERENCE && d->semantics != EVT_VIT_STANDARD)
     return fail(EVT_EINVAL, "semantics must be EVT_VIT_REFERENCE or EVT_VIT_STANDARD");
@@ -249,9 +251,15 @@ int validate(const evt_vit_desc* d, Shape* sh) {
   sh->max_ffn_st = 0;
   for (int i = 0; i < d->depth; ++i) {
     if (d->heads[i] <= 0) return fail(EVT_EINVAL, "heads per layer must be positive");
-    if (d->head_dim[i] != 64) return fail(EVT_EINVAL, "head size must be 64 in this build");
+    // any h_k (attention.py:6-12) up to 128; 64 runs the tuned kernels, others the generic ones
+    if (d->head_dim[i] <= 0 || d->head_dim[i] > 128)
+      return fail(EVT_EINVAL, "head size must be in [1, 128]");
+    if (d->heads[i] * d->head_dim[i] % 8)
+      return fail(EVT_EINVAL, "heads * head size must be a multiple of 8 (16-B token rows)");
+    if (d->dtype == EVT_DTYPE_MX8 && d->head_dim[i] != 64)
+      return fail(EVT_EINVAL, "EVT_DTYPE_MX8 supports head size 64 only");
     if (d->ffn[i] <= 0) return fail(EVT_EINVAL, "ffn width per layer must be positive");
-    sh->max_inner = std::max(sh->max_inner, d->heads[i] * 64);
+    sh->max_inner = std::max(sh->max_inner, d->heads[i] * d->head_dim[i]);
     sh->max_ffn_st = std::max<int>(sh->max_ffn_st, (int)round_up(d->ffn[i], PAD_N));
   }
   sh->head_st = (int)round_up(d->mlp_dim, PAD_N);
@@ -452,7 +460,8 @@ int build_encoder(evt_model* m, const float* const* w, hipStream_t s) {
   for (int i = 0; i < depth; ++i) {
     Layer& L = m->layers[i];
     L.heads = m->heads[i];
-    L.inner = L.heads * 64;
+    L.hd = m->head_dim[i];
+    L.inner = L.heads * L.hd;
     L.ffn = m->ffn[i];
     L.ffn_st = (int)round_up(L.ffn, PAD_N);
     EVT_RC(copy_vec(m, &L.ln1_g, w[k + 0], D, s));
@@ -513,13 +522,21 @@ int alloc_encoder_ws(evt_model* m, int B, size_t hbuf_bytes, hipStream_t s) {
     EVT_HIP(hipMemsetAsync(m->sk, 0, 4096, s), "memset stream-K flags");
   }
   const size_t rows = (size_t)B * m->sh.T;
-  EVT_RC(dev_alloc(m, &m->x, rows * m->D * es));
-  EVT_RC(dev_alloc(m, &m->xm, rows * m->D * es));
+  // x, xm (width D) and o (width heads * h_k) are GEMM A operands read in 64-column K-tiles: with
+  // a width that is not a multiple of 64 a row's last K-tile runs into the next row (cancelled by
+  // the zero-padded weight rows) and the last row into PAD_K zeroed slack elements; every byte is
+  // zeroed once here (finite everywhere)
+  const size_t xb = (rows * m->D + PAD_K) * es, ob = (rows * m->sh.max_inner + PAD_K) * es;
+  EVT_RC(dev_alloc(m, &m->x, xb));
+  EVT_RC(dev_alloc(m, &m->xm, xb));
   const size_t stats_bytes = rows * stats_slots(m->D) * 2 * sizeof(float);
   EVT_RC(dev_alloc(m, (void**)&m->sx, stats_bytes));
   EVT_RC(dev_alloc(m, (void**)&m->sm, stats_bytes));
   EVT_RC(dev_alloc(m, &m->qkv, rows * 3 * m->sh.max_inner * es));
-  EVT_RC(dev_alloc(m, &m->o, rows * m->sh.max_inner * es));
+  EVT_RC(dev_alloc(m, &m->o, ob));
+  EVT_HIP(hipMemsetAsync(m->x, 0, xb, s), "memset x");
+  EVT_HIP(hipMemsetAsync(m->xm, 0, xb, s), "memset xm");
+  EVT_HIP(hipMemsetAsync(m->o, 0, ob, s), "memset o");
   EVT_RC(dev_alloc(m, &m->hbuf, hbuf_bytes));
   m->hbuf_bytes = hbuf_bytes;
   m->chain.sync_bytes = ((rows + 255) / 256 + 3) * 4 + 16;
@@ -553,9 +570,11 @@ int dense_head(const evt_model* m, const DenseW& w, const DenseCall& c, hipStrea
 int run_encoder(evt_model* m, int B, hipStream_t s) {
   const int D = m->D, T = m->sh.T, rows = B * T;
   const float log2e = 1.4426950408889634f;
-  const bool fuse = m->dtype == DT_BF16 && D % 64 == 0 && qkv_attn_supported(T, D) &&
-                    (m->fusion & EVT_FUSE_QKV_ATTENTION) != 0;
+  const bool fuse_on = m->dtype == DT_BF16 && D % 64 == 0 && qkv_attn_supported(T, D) &&
+                       (m->fusion & EVT_FUSE_QKV_ATTENTION) != 0;
   for (const Layer& L : m->layers) {
+    const bool fuse = fuse_on && L.hd == 64;
+    const float scale_log2 = log2e / std::sqrt((float)L.hd);  // h_k^-0.5 (attention.py:13)
     if (fuse) {  // LN1-folded QKV + attention in one kernel (qkv_attn.hip)
       ProfScope ps(m, EVT_PROF_QKV_ATTENTION, s);
       prof_work(m, 2.0 * rows * D * 3 * L.inner + 4.0 * B * L.heads * (double)T * T * 64,
@@ -578,9 +597,10 @@ int run_encoder(evt_model* m, int B, hipStream_t s) {
         EVT_RC(dense(m, L.qkv, c, s));
       }
       ProfScope ps(m, EVT_PROF_ATTENTION, s);
-      prof_work(m, 4.0 * B * L.heads * (double)T * T * 64,
+      prof_work(m, 4.0 * B * L.heads * (double)T * T * L.hd,
                 (double)rows * 4 * L.inner * elem_size(m->dtype));  // qkv read + O written
-      AttnParams ap{m->qkv, 3 * L.inner, m->o, L.inner, T, L.heads, B, 0.125f * log2e};
+      AttnParams ap{m->qkv, 3 * L.inner, m->o, L.inner, T, L.heads, B, scale_log2};
+      ap.hd = L.hd;
       EVT_HIP(attention_launch(m->dtype, ap, s), "attention");
     }
     // out-proj + bias + LN1(x) residual -> xm (+ stats); STANDARD: + x
@@ -680,11 +700,11 @@ int validate_t2t(const evt_t2t_desc* d, T2TShape* ts) {
     return fail(EVT_EINVAL, "image_size must be a positive multiple of 16");
   if (d->in_chans <= 0 || d->num_classes <= 0 || d->depth < 0 || d->mlp_dim <= 0)
     return fail(EVT_EINVAL, "in_chans, num_classes, mlp_dim must be positive, depth >= 0");
-  if (d->dim <= 0 || d->dim % 64 != 0 || d->dim > 1024)
-    return fail(EVT_EINVAL, "dim must be a positive multiple of 64 and <= 1024");
+  if (d->dim <= 0 || d->dim % 8 != 0 || d->dim > 1024)
+    return fail(EVT_EINVAL, "dim must be a positive multiple of 8 and <= 1024");
   if (d->heads <= 0 || d->dim % d->heads != 0)  // Attention raises ValueError (attention.py:8-9)
     return fail(EVT_EINVAL, "hidden_size must be a multiple of num_heads");
-  if (d->dim / d->heads != 64) return fail(EVT_EINVAL, "head size must be 64 in this build");
+  if (d->dim / d->heads > 128) return fail(EVT_EINVAL, "head size (dim / heads) must be <= 128");
   if (d->token_size != 64) return fail(EVT_EINVAL, "token_size must be 64 in this build");
   if (d->max_batch <= 0) return fail(EVT_EINVAL, "max_batch must be positive");
   const int S = d->image_size;
@@ -699,7 +719,7 @@ int validate_t2t(const evt_t2t_desc* d, T2TShape* ts) {
   if (sh.T > 256) return fail(EVT_EINVAL, "at most 255 patches per image are supported");
   sh.D = d->dim;
   sh.pd = 9 * 64;
-  sh.max_inner = d->heads * 64;
+  sh.max_inner = d->dim;  // heads * (dim / heads)
   sh.max_ffn_st = (int)round_up(d->mlp_dim, PAD_N);
   sh.head_st = 0;
   return EVT_OK;
@@ -1024,7 +1044,7 @@ int evt_t2t_create(const evt_t2t_desc* desc, const float* const* w, int n_weight
   m->num_classes = desc->num_classes;
   m->tdesc = *desc;
   m->heads.assign(desc->depth, desc->heads);
-  m->head_dim.assign(desc->depth, 64);
+  m->head_dim.assign(desc->depth, desc->dim / desc->heads);  // h_k = dim // heads
   m->ffn.assign(desc->depth, desc->mlp_dim);
   m->sh = ts.enc;
   for (int i = 0; i < 3; ++i) m->grid[i] = ts.grid[i];
@@ -1791,6 +1811,25 @@ int evt_dense_splitk(int dtype, const evt_dense_args* a, int splits, float* part
   hipError_t e = gemm_splitk_launch(dtype, a->flags, p, splits, partials, (hipStream_t)stream);
   if (e == hipErrorInvalidValue) return fail(EVT_EINVAL, "dense_splitk: unsupported flags/shape");
   EVT_HIP(e, "dense_splitk");
+  return EVT_OK;
+}
+
+int evt_attention_hd(int dtype, const void* qkv, int64_t ldq, void* out, int64_t ldo, int B,
+                     int N, int H, int head_dim, float scale, void* stream) {
+  if (!qkv || !out || B < 0 || N <= 0 || N > 256 || H <= 0 || head_dim <= 0 || head_dim > 128 ||
+      ldq < 3 * (int64_t)H * head_dim || ldo < (int64_t)H * head_dim)
+    return fail(EVT_EINVAL, "attention: bad shape (N <= 256, head size in [1, 128])");
+  // vector accesses: 16-B loads of q / k / v rows when h_k is a multiple of 16 B, 4-element stores
+  // of O when h_k % 4 == 0 (head size 64: the tuned kernels' 16-B loads and stores)
+  const int64_t vec = dtype == DT_BF16 ? 8 : 4;
+  const bool vload = head_dim % vec == 0, vstore = head_dim % 4 == 0;
+  if (vload && (ldq % vec || ((uintptr_t)qkv & 15)))
+    return fail(EVT_EINVAL, "attention: qkv rows must be 16-B aligned for this head size");
+  if ((vstore || head_dim == 64) && (ldo % (head_dim == 64 ? vec : 4) || ((uintptr_t)out & 15)))
+    return fail(EVT_EINVAL, "attention: out rows must be 16-B aligned for this head size");
+  AttnParams p{qkv, ldq, out, ldo, N, H, B, scale * 1.4426950408889634f};
+  p.hd = head_dim;
+  EVT_HIP(attention_launch(dtype, p, (hipStream_t)stream), "attention");
   return EVT_OK;
 }
 

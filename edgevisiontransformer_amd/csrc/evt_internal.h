@@ -103,7 +103,7 @@ struct AttnParams {
   const void* qkv; int64_t ldq;   // token rows, columns (qkv h d)
   void* out;       int64_t ldo;   // token rows, columns (h d)
   int N;                          // tokens per image (<= 256)
-  int H;                          // heads; head_dim is fixed at 64
+  int H;                          // heads
   int B;                          // images
   float scale_log2;               // head_dim^-0.5 * log2(e)
   // bf16 only: when q8 is set, O is written as MX8 instead (e4m3 bytes q8[row][ldq8], scales
@@ -112,6 +112,7 @@ struct AttnParams {
   uint32_t* s8 = nullptr;
   int64_t ldq8 = 0;
   int rows8 = 0;
+  int hd = 64;                    // head size h_k (<= 128; 64: the tuned kernels, else generic)
 };
 hipError_t attention_launch(int dtype, const AttnParams& p, hipStream_t s);
 

@@ -13,7 +13,7 @@ t2t_vit.py:50-52): fp32 NHWC [B, S, S, 3]. Deliberate differences, as for ViT: `
 `weights=` select the parameters (the reference random-initialises, t2t_vit.py:116-118), and
 `dtype` selects the bf16 MFMA path or the exact fp32 path. Unsupported reference options fail
 loudly: tokens_type other than 'performer' raises NotImplementedError (t2t_vit.py:58-59),
-token_size must be 64, hidden_size / num_heads must be 64.
+token_size must be 64, the head size hidden_size // num_heads at most 128.
 """
 from __future__ import annotations
 

@@ -187,7 +187,7 @@ class T2TConfig:
     num_classes: int = 1000
     dim: int = 384                # hidden_size
     depth: int = 14
-    heads: int = 6                # num_heads (head size dim / heads = 64)
+    heads: int = 6                # num_heads (head size h_k = dim // heads)
     mlp_dim: int = 1152           # int(mlp_ratio * hidden_size) (t2t_vit.py:110)
     token_size: int = 64
 
@@ -254,7 +254,7 @@ def t2t_param_shapes(cfg: T2TConfig) -> List[tuple]:
     out += [("project_w", (cfg.split_dims[2], d)), ("project_b", (d,)), ("cls", (d,)),
             ("pos", (cfg.tokens, d))]
     for i in range(cfg.depth):
-        inner = cfg.heads * 64
+        inner = cfg.heads * (d // cfg.heads)  # Attention(hidden_size, num_heads): h_k = d // heads
         out += [(f"l{i}.ln1_g", (d,)), (f"l{i}.ln1_b", (d,)),
                 (f"l{i}.qkv_w", (d, 3 * inner)),
                 (f"l{i}.out_w", (inner, d)), (f"l{i}.out_b", (d,)),

@@ -51,11 +51,11 @@ typedef struct evt_vit_desc {
   int32_t patch_size;   /* 16; image_size % patch_size == 0 (vit.py:13) */
   int32_t in_chans;     /* 3 */
   int32_t num_classes;  /* 1000 */
-  int32_t dim;          /* D: 192 / 384 / 768; multiple of 64, <= 1024 */
+  int32_t dim;          /* D: 192 / 384 / 768; multiple of 8, <= 1024 (MX8: of 64) */
   int32_t depth;        /* 12 */
   int32_t mlp_dim;      /* head MLP width M (vit.py:38) */
   const int32_t* heads;    /* [depth] heads per layer (attention.py:5) */
-  const int32_t* head_dim; /* [depth] h_k per layer; this build requires 64 */
+  const int32_t* head_dim; /* [depth] h_k per layer, in [1, 128]; heads * h_k % 8 == 0 (MX8: 64) */
   const int32_t* ffn;      /* [depth] FFN width per layer (ffn.py:5) */
   int32_t dtype;        /* EVT_DTYPE_* */
   int32_t max_batch;    /* workspace is sized for this many images */
@@ -257,6 +257,12 @@ int evt_qkv_attention(const void* x, int D, const float* stats, const void* Wp, 
 int evt_attention(int dtype, const void* qkv, int64_t ldq, void* out, int64_t ldo, int B, int N,
                   int H, float scale, void* stream);
 
+/* evt_attention for any head size h_k = head_dim in [1, 128] (attention.py:6-12: h_k = dim //
+ * heads): qkv [B*N, ldq >= 3*H*h_k] columns (qkv h d), out [B*N, ldo >= H*h_k] columns (h d).
+ * h_k == 64 runs the tuned kernels, other sizes generic ones (features zero-padded to 32 / 64). */
+int evt_attention_hd(int dtype, const void* qkv, int64_t ldq, void* out, int64_t ldo, int B, int N,
+                     int H, int head_dim, float scale, void* stream);
+
 /* LayerNormalization(epsilon) over rows of D (norm.py:6): fp32 x -> y (dtype). */
 int evt_layernorm(int dtype, const float* x, int64_t ldx, void* y, int64_t ldy,
                   const float* gamma, const float* beta, int rows, int D, float eps, void* stream);
@@ -284,9 +290,9 @@ typedef struct evt_t2t_desc {
   int32_t image_size;   /* S = 224 */
   int32_t in_chans;     /* 3 */
   int32_t num_classes;  /* 1000 */
-  int32_t dim;          /* hidden_size: multiple of 64, <= 1024 */
+  int32_t dim;          /* hidden_size: multiple of 8, <= 1024 */
   int32_t depth;        /* encoder layers */
-  int32_t heads;        /* num_heads; dim / heads must be 64 */
+  int32_t heads;        /* num_heads; h_k = dim / heads <= 128 (attention.py:6-12) */
   int32_t mlp_dim;      /* int(mlp_ratio * hidden_size) */
   int32_t token_size;   /* TokenPerformer head size; this build requires 64 (m = 32) */
   int32_t dtype;        /* EVT_DTYPE_* */

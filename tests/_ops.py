@@ -87,6 +87,18 @@ def attention(dtype, qkv, B, N, H, scale=0.125, out=None):
     return out
 
 
+def attention_hd(dtype, qkv, B, N, H, hd, scale=None, out=None):
+    """evt_attention_hd: any head size hd (attention.py:6-12); scale defaults to hd^-0.5."""
+    if out is None:
+        out = torch.zeros((B * N, H * hd), dtype=TDT[dtype], device=qkv.device)
+    if scale is None:
+        scale = hd ** -0.5
+    _lib.check(_lib.load_library().evt_attention_hd(_lib.DTYPE[dtype], _p(qkv), qkv.stride(0),
+                                                    _p(out), out.stride(0), B, N, H, hd, scale,
+                                                    _s()))
+    return out
+
+
 def layernorm(dtype, x, gamma, beta, eps=1e-5):
     rows, D = x.shape
     y = torch.empty((rows, D), dtype=TDT[dtype], device=x.device)

@@ -2,7 +2,7 @@
 
 Run in the build container only (it needs /root/reference, which never reaches the GPU box):
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [case ...]
 
 What it does
 ------------
@@ -158,7 +158,8 @@ def t2t_reference_forward(params, cfg, img, trace=None):
         x = x @ _t(params["project_w"]) + _t(params["project_b"])
         cls = _t(params["cls"]).reshape(1, 1, d).expand(x.shape[0], 1, d)
         x = torch.cat([cls, x], dim=1) + _t(params["pos"])
-        x = ref_encoder(x, params, d, [cfg.heads] * cfg.depth, [64] * cfg.depth,
+        # TransformerEncoderBlock -> Attention(hidden_size, num_heads): h_k = dim // heads
+        x = ref_encoder(x, params, d, [cfg.heads] * cfg.depth, [d // cfg.heads] * cfg.depth,
                         [cfg.mlp_dim] * cfg.depth, trace)
         t = torch.nn.functional.layer_norm(x[:, 0], (d,), _t(params["norm_g"]),
                                            _t(params["norm_b"]), eps=1e-5)
@@ -170,6 +171,8 @@ def t2t_reference_forward(params, cfg, img, trace=None):
 T2T_CASES = {
     "t2t_vit_7_b2": ((256, 7, 4, 2), 2, 11, 12),
     "t2t_vit_14_b1": ((384, 14, 6, 3), 1, 13, 14),
+    # head size 96 (T2T_ViT(hidden_size=384, num_heads=4)): the generic attention kernels
+    "t2t_384h4_d2_b1": ((384, 2, 4, 3), 1, 15, 16),
 }
 
 
@@ -181,6 +184,12 @@ CASES = {
     "vit_small2_layerwise_b3": (dict(dim=128, depth=2, heads=2, mlp_dim=320, num_classes=37),
                                 "layerwise_h1-d0.37_h3-d0.1", 3, 5, 6),
     "deit_base_b1": (dict(dim=768, depth=12, heads=12, mlp_dim=3072), None, 1, 7, 8),
+    # head sizes other than 64 (attention.py:6-12, h_k = dim // heads) and widths that are not a
+    # multiple of 64: Attention(96, 1), Attention(768, 8), h_k 32, and h_k 10 with D = 80
+    "vit_d96_h1_b2": (dict(dim=96, depth=2, heads=1, mlp_dim=192, num_classes=10), None, 2, 17, 18),
+    "vit_d768_h8_b1": (dict(dim=768, depth=2, heads=8, mlp_dim=1536), None, 1, 19, 20),
+    "vit_d192_h6_b2": (dict(dim=192, depth=3, heads=6, mlp_dim=384), None, 2, 21, 22),
+    "vit_d80_h8_b2": (dict(dim=80, depth=2, heads=8, mlp_dim=160, num_classes=7), None, 2, 23, 24),
 }
 
 
@@ -198,8 +207,10 @@ def case_config(name):
     return vit_config(**kw, head_size=64, heads_list=hl, ffn_list=fl)
 
 
-def main():
+def main(only=()):
     for name, (kw, enc, batch, pseed, iseed) in CASES.items():
+        if only and name not in only:
+            continue
         cfg = case_config(name)
         params = make_vit_params(cfg, seed=pseed)
         img = make_images(batch, seed=iseed, image_size=cfg.image_size)
@@ -213,6 +224,8 @@ def main():
             encoding=enc or "")
         print(f"{name}: logits {logits.shape} absmax {np.abs(logits).max():.4f} -> {path}")
     for name, (args, batch, pseed, iseed) in T2T_CASES.items():
+        if only and name not in only:
+            continue
         cfg = t2t_config(*args)
         params = make_t2t_params(cfg, seed=pseed)
         img = make_images(batch, seed=iseed, image_size=cfg.image_size, layout="NHWC")
@@ -228,4 +241,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))  # optional case names: regenerate only those

@@ -27,7 +27,7 @@ def lib():
 def test_header_and_binding_agree():
     from edgevisiontransformer_amd import _lib
     assert _declared() == sorted(_lib.SIGNATURES)
-    assert len(_declared()) == 44
+    assert len(_declared()) == 45
 
 
 def test_every_declared_symbol_is_exported(lib):
@@ -48,9 +48,15 @@ def test_host_validation_codes(lib):
     bad = _lib.evt_vit_desc(225, 16, 3, 1000, 768, 12, 3072, arr, hd, ffn, 1, 512)
     assert lib.evt_query_workspace(ctypes.byref(bad), 512, ctypes.byref(out)) == _lib.EVT_EINVAL
     assert b"divisible by the patch size" in lib.evt_last_error()
-    hd2 = (ctypes.c_int32 * 12)(*([32] * 12))
-    bad2 = _lib.evt_vit_desc(224, 16, 3, 1000, 768, 12, 3072, arr, hd2, ffn, 1, 512)
+    hd2 = (ctypes.c_int32 * 12)(*([32] * 12))  # any head size in [1, 128] is accepted
+    ok2 = _lib.evt_vit_desc(224, 16, 3, 1000, 768, 12, 3072, arr, hd2, ffn, 1, 512)
+    assert lib.evt_query_workspace(ctypes.byref(ok2), 1, ctypes.byref(out)) == 0
+    hd3 = (ctypes.c_int32 * 12)(*([160] * 12))
+    bad2 = _lib.evt_vit_desc(224, 16, 3, 1000, 768, 12, 3072, arr, hd3, ffn, 1, 512)
     assert lib.evt_query_workspace(ctypes.byref(bad2), 1, ctypes.byref(out)) == _lib.EVT_EINVAL
+    assert b"head size" in lib.evt_last_error()
+    bad3 = _lib.evt_vit_desc(224, 16, 3, 1000, 100, 12, 3072, arr, hd, ffn, 1, 512)
+    assert lib.evt_query_workspace(ctypes.byref(bad3), 1, ctypes.byref(out)) == _lib.EVT_EINVAL
     out_h = ctypes.c_void_p()
     assert lib.evt_vit_create(ctypes.byref(d), None, 0, None, ctypes.byref(out_h)) == _lib.EVT_EINVAL
     assert lib.evt_model_destroy(None) == 0

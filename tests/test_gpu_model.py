@@ -107,7 +107,11 @@ def test_errors_are_loud(gpu):
     with pytest.raises(AssertionError):
         ViT(image_size=225, patch_size=16)
     with pytest.raises(EvtError):
-        ViT(dim=96, heads=1, mlp_dim=96, depth=1, device=gpu, max_batch=1)  # dim % 64 != 0
+        ViT(dim=100, heads=1, mlp_dim=96, depth=1, device=gpu, max_batch=1)  # dim % 8 != 0
+    with pytest.raises(EvtError):
+        ViT(dim=256, heads=1, mlp_dim=96, depth=1, device=gpu, max_batch=1)  # h_k 256 > 128
+    with pytest.raises(EvtError):
+        ViT(dim=96, heads=1, mlp_dim=96, depth=1, dtype="mx8", device=gpu, max_batch=1)  # MX8: 64
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f32"])

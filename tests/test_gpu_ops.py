@@ -186,6 +186,34 @@ def test_attention(gpu, dtype, B, N, H):
     torch.testing.assert_close(out.double().cpu(), ref, **tol)
 
 
+def _attn_ref_hd(qkv64, B, N, H, hd):
+    q, k, v = qkv64.reshape(B, N, 3, H, hd).permute(2, 0, 3, 1, 4)
+    s = torch.einsum("bhid,bhjd->bhij", q, k) * hd ** -0.5
+    p = torch.softmax(s, dim=-1)
+    return torch.einsum("bhij,bhjd->bhid", p, v).permute(0, 2, 1, 3).reshape(B * N, H * hd)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("B,N,H,hd", [(2, 197, 1, 96), (1, 197, 8, 96), (2, 197, 6, 32),
+                                      (2, 197, 8, 10), (1, 50, 3, 128), (3, 129, 2, 48),
+                                      (1, 256, 2, 72), (2, 1, 4, 24), (1, 64, 5, 100),
+                                      (2, 197, 2, 64)])
+def test_attention_any_head_size(gpu, dtype, B, N, H, hd):
+    """evt_attention_hd against a torch fp64 attention of the same rounded inputs: h_k other than
+    64 (the generic kernels, features zero-padded to 32 / 64; odd sizes take the element-wise
+    paths), 64 (the tuned kernels through the same entry point)."""
+    qkv64 = _rand((B * N, 3 * H * hd), 13, scale=1.5)
+    qkv = qkv64.to(_ops.TDT[dtype]).to(gpu)
+    full = torch.full((B * N, H * hd + 8), 7.0, dtype=_ops.TDT[dtype], device=gpu)
+    out = full[:, : H * hd]
+    _ops.attention_hd(dtype, qkv, B, N, H, hd, out=out)
+    torch.cuda.synchronize()
+    ref = _attn_ref_hd(_q(qkv64, dtype), B, N, H, hd)
+    tol = dict(rtol=2e-2, atol=2e-2) if dtype == "bf16" else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(out.double().cpu(), ref, **tol)
+    assert torch.all(full[:, H * hd:] == 7.0), "columns past H * h_k must stay untouched"
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "f32"])
 def test_attention_peaked_softmax(gpu, dtype):
     """One key dominates every query (scores ~ +40): exercises the max-subtraction path."""

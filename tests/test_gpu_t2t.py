@@ -165,4 +165,4 @@ def test_t2t_errors_are_loud(gpu):
     with pytest.raises(ValueError):
         T2T_ViT(hidden_size=256, num_heads=3, device=gpu)
     with pytest.raises(_lib.EvtError):
-        T2T_ViT(hidden_size=384, depth=1, num_heads=4, device=gpu, max_batch=1)  # head size 96
+        T2T_ViT(hidden_size=384, depth=1, num_heads=2, device=gpu, max_batch=1)  # head size 192
