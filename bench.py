@@ -27,8 +27,9 @@ Extra objects on the JSON line:
                 gemm_pers_kernel<35> launches); achieved = its algorithmic FLOPs (or bytes, for
                 an HBM-bound role) / avg launch time vs the 2.5 PF dense bf16 MFMA peak (8 TB/s
                 HBM); hbm_frac = algorithmic bytes / time / 8 TB/s for every role (per_role);
-                traffic = HBM bytes per launch from the rocprofv3 PMC pass committed in
-                profiles/pmc_fc1.json (its build commit is reported beside it).
+                traffic = HBM bytes per launch of the same role in real forwards of the same
+                configuration, from the rocprofv3 PMC passes committed as
+                profiles/pmc_<model>_<dtype>_bs<batch>.json (build commit reported beside it).
   cpu_baseline  the numpy fp32 restatement of the reference forward (oracle/, "port": TF is not
                 installed anywhere), bs=1 forwards of the same model for ~15 s on the host BLAS
                 threads.
@@ -51,11 +52,21 @@ sys.path.insert(0, REPO)
 PEAK_BF16_TFLOPS = 2516.6   # MI355X dense bf16 MFMA (spec; MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3     # MI355X fp32 matrix (spec)
 PEAK_HBM_GBPS = 8000.0      # MI355X HBM3E (spec; MI355X_MICROARCH.md)
-PMC_FILE = os.path.join(REPO, "profiles", "pmc_fc1.json")
-KERNEL_NAMES = {"fc1": "gemm_pers_kernel<LNIN|BIAS|GELU> (FC1)", "fc2": "gemm_pers_kernel<BIAS|RESID|RESLN|STATS> (FC2)",
-                "qkv": "gemm_pers_kernel<LNIN|BIAS> (QKV)", "attention": "attn_bf16_kernel",
-                "mlp": "swin_mlp96_kernel (stage-1 fused MLP)",
-                "attn_sublayer": "swin_attn96_kernel (stage-1 fused attention sublayer)"}
+PMC_DIR = os.path.join(REPO, "profiles")  # pmc_<model>_<dtype>_bs<batch>.json (scripts/gpu_r4_pmc.sh)
+def kernel_label(model: str, dtype: str, role: str) -> str:
+    """The kernels a role's launches run (persistent 256x256 GEMM where the tile count fills the
+    chip, else the 128x128 one; the fp32 path always the latter)."""
+    swin = model.startswith("swin")
+    gemm = "gemm_pers_kernel / gemm_nt_kernel" if dtype == "bf16" else "gemm_nt_kernel<float>"
+    res = "BIAS|RESID|STATS" if swin else "BIAS|RESID|RESLN|STATS"
+    names = {"fc1": f"{gemm}<LNIN|BIAS|{'GELU_ERF' if swin else 'GELU'}> (FC1)",
+             "fc2": f"{gemm}<{res}> (FC2)", "out_proj": f"{gemm}<{res}> (out-proj)",
+             "qkv": f"{gemm}<LNIN|BIAS> (QKV)",
+             "attention": ("window_attn_bf16_kernel" if swin else
+                           "attn_bf16_kernel" if dtype == "bf16" else "attn_f32_kernel"),
+             "mlp": "swin_mlp96_kernel (stage-1 fused MLP)",
+             "attn_sublayer": "swin_attn96_kernel (stage-1 fused attention sublayer)"}
+    return names.get(role, role)
 METRIC = "images/sec DeiT-base/16-224 bs=512 @1/2/4/8 GPU; % bf16 MFMA roofline"
 
 
@@ -174,18 +185,20 @@ def cpu_baseline(model_name: str, budget_s: float) -> dict:
                       f"({src}) in {el:.1f} s; reference TF-CPU path not installable"}
 
 
-def pmc_traffic(M: int, K: int, N: int):
-    """HBM bytes per launch of the FC1 kernel from the rocprofv3 PMC pass committed as
-    profiles/pmc_fc1.json (scripts/gpu_pmc_fc1.sh: 2 x FETCH_SIZE, gfx950 tallies 128-B requests
-    at 64 B, MI355X_MICROARCH.md HBM section, + WRITE_SIZE) and the build commit it measured.
-    None if absent or collected at another shape."""
+def pmc_traffic(model: str, dtype: str, batch: int, role: str):
+    """HBM bytes per launch of `role`'s kernels in real forwards of this configuration, from the
+    rocprofv3 PMC passes committed as profiles/pmc_<model>_<dtype>_bs<batch>.json
+    (scripts/gpu_r4_pmc.sh + scripts/pmc_roles.py: 2 x FETCH_SIZE, gfx950 tallies 128-B requests
+    at 64 B, MI355X_MICROARCH.md HBM section, + WRITE_SIZE, averaged over the role's launches) and
+    the build commit it measured. None if absent or collected for another role."""
+    f = os.path.join(PMC_DIR, f"pmc_{model}_{dtype}_bs{batch}.json")
     try:
-        d = json.load(open(PMC_FILE))
+        d = json.load(open(f))
     except Exception:
         return None, None
-    if (d.get("M"), d.get("K"), d.get("N")) != (M, K, N):
+    if d.get("role") != role or d.get("batch") != batch:
         return None, None
-    return d.get("traffic_bytes_per_launch"), {"file": os.path.relpath(PMC_FILE, REPO),
+    return d.get("traffic_bytes_per_launch"), {"file": os.path.relpath(f, REPO),
                                                "commit": d.get("commit"),
                                                "collected": d.get("collected")}
 
@@ -296,7 +309,7 @@ def main():
                 "unit": "TFLOP/s" if mfma_bound else "GB/s",
                 "frac": round(ach / (peak if mfma_bound else PEAK_HBM_GBPS), 4),
                 "traffic": None, "role": dom,
-                "kernel": f"{KERNEL_NAMES.get(dom, dom)} ({args.model}, {args.dtype})",
+                "kernel": f"{kernel_label(args.model, args.dtype, dom)} ({args.model}, {args.dtype})",
                 "algorithmic_flop_per_launch": fl, "algorithmic_bytes_per_launch": by,
                 "hbm_gbps": round(by / t_k / 1e9, 1),
                 "hbm_frac": round(by / t_k / 1e9 / PEAK_HBM_GBPS, 4),
@@ -305,10 +318,10 @@ def main():
                 "timing": "HIP events around each launch of the role inside 5 forwards "
                           "(evt_model_profile) of the kernels the timed forwards run",
                 "per_role": table}
+        roof["traffic"], roof["traffic_source"] = pmc_traffic(args.model, args.dtype, cap, dom)
         if dom == "fc1" and not t2t and not swin:
             M, K, N = B * model.cfg.tokens, model.cfg.dim, model.cfg.ffn[0]
             roof["kernel"] += f" M={M} K={K} N={N}"
-            roof["traffic"], roof["traffic_source"] = pmc_traffic(M, K, N)
             if args.isolated_probe:  # off by default: its launches would mix into a rocprof average
                 roof["isolated_probe_us"] = round(kernel_probe(args.dtype, M, K, N) * 1e6, 1)
     cpu = None
