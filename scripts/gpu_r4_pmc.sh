@@ -9,6 +9,7 @@ O=$R/gpurun_out/${TAG:-r4pmc}
 mkdir -p $O
 while read -r NAME ROLE ARGS; do
   [ -z "$NAME" ] && continue
+  if [ -n "${ONLY:-}" ] && ! echo " $ONLY " | grep -q " $NAME "; then continue; fi
   mkdir -p $O/$NAME
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d $O/$NAME/$C -o run \

@@ -15,17 +15,18 @@ import json
 import os
 import sys
 
-# (model family, dtype) -> role -> [(kernel-name substring, modulus, remainder)]
+# (model family, dtype) -> role -> [(kernel-name substring, modulus, remainder)]; rocprofv3
+# demangles the float instantiations but not the bf16 (DF16b) ones of gemm_nt_kernel
 RULES = {
     ("vit", "bf16"): {"fc1": [("gemm_pers_kernel<35,", 1, 0)],
                       "qkv": [("gemm_pers_kernel<33,", 1, 0)],
                       "out_proj": [("gemm_pers_kernel<197,", 2, 0), ("gemm_nt_kernelIDF16bLi197E", 2, 0)],
                       "fc2": [("gemm_pers_kernel<197,", 2, 1), ("gemm_nt_kernelIDF16bLi197E", 2, 1)],
                       "attention": [("attn_bf16_kernel", 1, 0)]},
-    ("vit", "f32"): {"fc1": [("gemm_nt_kernelIfLi35E", 1, 0)],
-                     "qkv": [("gemm_nt_kernelIfLi33E", 1, 0)],
-                     "out_proj": [("gemm_nt_kernelIfLi197E", 2, 0)],
-                     "fc2": [("gemm_nt_kernelIfLi197E", 2, 1)],
+    ("vit", "f32"): {"fc1": [("gemm_nt_kernel<float, 35>", 1, 0)],
+                     "qkv": [("gemm_nt_kernel<float, 33>", 1, 0)],
+                     "out_proj": [("gemm_nt_kernel<float, 197>", 2, 0)],
+                     "fc2": [("gemm_nt_kernel<float, 197>", 2, 1)],
                      "attention": [("attn_f32_kernel", 1, 0)]},
     ("t2t", "bf16"): {"fc1": [("gemm_pers_kernel<35,", 1, 0)],
                       "out_proj": [("gemm_pers_kernel<197,", 2, 0)],
