@@ -494,7 +494,7 @@ constexpr int BIG_STAGE = 2 * BIG_TILE;       // 64 KiB per K-tile
 
 // evt_set_gemm_variant, per calling thread (launch decisions are made on the launching thread):
 // 0 auto, 1 force 128x128, 2 / 6 / 8 non-persistent 256x256 main loops, 9 tile-persistent,
-// 16 stream-K. Lab builds (-DEVT_GEMM_LAB) add the ablation / timeline / A-B variants 10, 11, 13,
+// 16 stream-K, 30 128 x 384 persistent wherever it applies, 31 automatic without it. Lab builds (-DEVT_GEMM_LAB) add the ablation / timeline / A-B variants 10, 11, 13,
 // 15, 17-25, 106, 108 used by scripts/gemm_bench.py and scripts/probe/pers_timeline.py.
 thread_local int g_gemm_variant = 0;
 // Lab A/B: -DEVT_EPI_PACK_FIRST=0 (persistent epilogue without residual: swap fp32 rows, then pack)
@@ -505,8 +505,9 @@ thread_local int g_gemm_variant = 0;
 bool use_big(const GemmParams& p, int flags) {
   if ((p.ntiles * GEMM_BN) % BIG_BN) return false;
   if (!(flags & EPI_OUT_F32) && p.vec_ok < 2) return false;  // big epilogue: 16-B bf16 stores only
-  if (g_gemm_variant == 1) return false;
-  if (g_gemm_variant >= 2) return true;
+  const int v = g_gemm_variant == 31 ? 0 : g_gemm_variant;  // 31: automatic without 128 x 384
+  if (v == 1) return false;
+  if (v >= 2) return true;
   // enough 256x256 tiles to fill the chip at least once
   return (int64_t)((p.M + 255) / 256) * (p.ntiles * GEMM_BN / 256) >= 256;
 }
@@ -610,6 +611,30 @@ __device__ __forceinline__ void big8_bar() {
 // (gmode 1) / the T2T soft split (gmode 2).
 struct MergeParams : GemmParams {};
 struct UnfoldParams : GemmParams {};
+// 128 x 384 tiles (gemm_p384_kernel): the params type selects the tile geometry at compile time
+struct P384Params : GemmParams {};
+
+// Tile geometry of the 8-phase main loop by params type: BM x BN block tile, 8 waves as 2 (wm) x 4
+// (wn), each wave (BM / 2) x (BN / 4) = MF x NF fragments of 16 x 16. The K-tile's LDS stage is
+// A (BM rows) then W (BN rows) of 128 B, 64 KiB for both geometries; its four DMA regions are the
+// A m-halves (AI instructions per wave) and the W n-halves (WI per wave), AI + WI = 4.
+template <typename P>
+struct GeoOf {
+  static constexpr int BM = 256, BN = 256, MF = 8, NF = 4;
+};
+template <>
+struct GeoOf<P384Params> {
+  static constexpr int BM = 128, BN = 384, MF = 4, NF = 6;
+};
+template <typename P>
+struct Geo : GeoOf<P> {
+  using G = GeoOf<P>;
+  static constexpr int WR = G::BM / 2, WC = G::BN / 4;  // wave tile rows / columns
+  static constexpr int MH = G::MF / 2, NH = G::NF / 2;  // fragments per m-half / n-half
+  static constexpr int A_TILE = G::BM * ROWB;
+  static constexpr int AI = G::BM / 128, WI = G::BN / 128;  // DMA instructions per wave per region
+  static_assert(A_TILE + G::BN * ROWB == BIG_STAGE && AI + WI == 4, "64 KiB K-tile stages");
+};
 
 // EPI_GATHER A address (Swin PatchMerging, reference SwinTransformer PatchMerging.forward:
 // x0 | x1 | x2 | x3 = x[0::2, 0::2] | x[1::2, 0::2] | x[0::2, 1::2] | x[1::2, 1::2]): GEMM row gm
@@ -645,9 +670,30 @@ __device__ __forceinline__ const char* gather_addr(const GemmParams& p, int gm, 
 template <typename P>
 __device__ __forceinline__ void big8_stage(const P& p, char* smem, int wave, int lane,
                                            int m0, int n0, int T, int j, int par = 0) {
+  typedef Geo<P> Gm;
   const int srow = lane >> 3, sslot = lane & 7;
   EVT_LDS char* base = (EVT_LDS char*)smem + ((T ^ par) & 1) * BIG_STAGE;
   const int64_t koff = (int64_t)T * ROWB + ((sslot ^ srow) << 4);
+  if constexpr (Gm::BM != 256) {  // general geometry: 8-row groups g of the region, in order
+    if (j == 0 || j == 3) {  // A m-half (j == 3): rows wm * WR + half * WR / 2 + [0, WR / 2)
+#pragma unroll
+      for (int i = 0; i < Gm::AI; ++i) {
+        const int g = wave * Gm::AI + i, gpw = Gm::WR / 16;  // groups per wave-row half
+        const int row = (g / gpw) * Gm::WR + (j == 3 ? Gm::WR / 2 : 0) + (g % gpw) * 8;
+        const int gm = min(m0 + row + srow, p.M - 1);
+        glds16((const char*)p.A + (int64_t)gm * (p.lda * 2) + koff, base + row * ROWB);
+      }
+    } else {  // W n-half (j == 2): rows wn * WC + half * WC / 2 + [0, WC / 2)
+#pragma unroll
+      for (int i = 0; i < Gm::WI; ++i) {
+        const int g = wave * Gm::WI + i, gpw = Gm::WC / 16;
+        const int row = (g / gpw) * Gm::WC + (j == 2 ? Gm::WC / 2 : 0) + (g % gpw) * 8;
+        glds16((const char*)p.W + (int64_t)(n0 + row + srow) * (p.ldw * 2) + koff,
+               base + Gm::A_TILE + row * ROWB);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int r = (wave * 2 + i) * 8;  // region row of this wave-instruction (8 rows)
@@ -694,40 +740,45 @@ __device__ __forceinline__ void big8_prologue(const P& p, char* smem, int wave, 
 // ph3: issues X3 further VMEM loads at the start of phase 3 (added to that phase's wait).
 template <int MODE, int X, bool OPEN = false, int X3 = 0, typename Ph3 = NoOp,
           typename P = GemmParams>
-__device__ __forceinline__ void big8_ktile(const P& p, char* smem, f32x4 (&acc)[4][8],
+__device__ __forceinline__ void big8_ktile(const P& p, char* smem,
+                                           f32x4 (&acc)[GeoOf<P>::NF][GeoOf<P>::MF],
                                            int wave, int lane, int wm, int wn, int m0, int n0,
                                            int t, bool cont = false, int nm0 = 0, int nn0 = 0,
                                            Ph3 ph3 = {}, int par = 0, int npar = 0,
                                            bool x3on = true) {
+  typedef Geo<P> Gm;
+  constexpr int MH = Gm::MH, NH = Gm::NH;
   const int frow = lane & 15, fsw = lane & 7, fg = lane >> 4;
   const EVT_LDS char* As = (const EVT_LDS char*)smem + ((t ^ par) & 1) * BIG_STAGE;
-  const EVT_LDS char* Ws = As + BIG_TILE;
+  const EVT_LDS char* Ws = As + Gm::A_TILE;
   auto rd = [&](const EVT_LDS char* S, int row, int ks) {
     return *(const EVT_LDS u32x4*)(S + row * ROWB + (((fg + 4 * ks) ^ fsw) << 4));
   };
-  u32x4 af[4][2], bf0[2][2], bf1[2][2];
+  u32x4 af[MH][2], bf0[NH][2], bf1[NH][2];
 #pragma unroll
   for (int ph = 0; ph < 4; ++ph) {
     auto reads = [&]() {
       if (ph == 0) {
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
+        for (int nt = 0; nt < NH; ++nt)
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) bf0[nt][ks] = rd(Ws, wn * 64 + nt * 16 + frow, ks);
+          for (int ks = 0; ks < 2; ++ks) bf0[nt][ks] = rd(Ws, wn * Gm::WC + nt * 16 + frow, ks);
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
+        for (int mt = 0; mt < MH; ++mt)
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) af[mt][ks] = rd(As, wm * 128 + mt * 16 + frow, ks);
+          for (int ks = 0; ks < 2; ++ks) af[mt][ks] = rd(As, wm * Gm::WR + mt * 16 + frow, ks);
       } else if (ph == 1) {
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
+        for (int nt = 0; nt < NH; ++nt)
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) bf1[nt][ks] = rd(Ws, wn * 64 + 32 + nt * 16 + frow, ks);
+          for (int ks = 0; ks < 2; ++ks)
+            bf1[nt][ks] = rd(Ws, wn * Gm::WC + Gm::WC / 2 + nt * 16 + frow, ks);
       } else if (ph == 2) {
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
+        for (int mt = 0; mt < MH; ++mt)
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) af[mt][ks] = rd(As, wm * 128 + 64 + mt * 16 + frow, ks);
+          for (int ks = 0; ks < 2; ++ks)
+            af[mt][ks] = rd(As, wm * Gm::WR + Gm::WR / 2 + mt * 16 + frow, ks);
       }
     };
     auto dmas = [&]() {
@@ -763,7 +814,7 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem, f32x4 (&acc)[
         if (ph == 3) wait_vm<4 + X>();
         else wait_vm<8 + X>();
       } else if (ph == 0) {
-        wait_vm<2 + X>();
+        wait_vm<Gm::AI + X>();  // the last K-tile's A m-half-1 region (j3) follows
       } else if (ph == 1) {
         wait_vm<0 + X>();
       }
@@ -776,13 +827,13 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem, f32x4 (&acc)[
 #if EVT_MFMA_PRIO == 1
     __builtin_amdgcn_s_setprio(1);
 #endif
-    const int mb = (ph >= 2) ? 4 : 0, nb = (ph == 1 || ph == 2) ? 2 : 0;
+    const int mb = (ph >= 2) ? MH : 0, nb = (ph == 1 || ph == 2) ? NH : 0;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
+      for (int nt = 0; nt < NH; ++nt)
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
+        for (int mt = 0; mt < MH; ++mt)
           Mma<bf16>::run(nb ? bf1[nt][ks] : bf0[nt][ks], af[mt][ks], acc[nb + nt][mb + mt]);
 #if EVT_MFMA_PRIO == 1
     __builtin_amdgcn_s_setprio(0);
@@ -803,7 +854,8 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem, f32x4 (&acc)[
 template <int X, bool OPEN = false, typename Pre1 = NoOp, typename Mid = NoOp, int LX = 0,
           typename Last = NoOp, int LX3 = 0, typename Last3 = NoOp, typename P = GemmParams,
           int PFX = 0, typename Pf = NoOp>
-__device__ __forceinline__ void big8_loop(const P& p, char* smem, f32x4 (&acc)[4][8],
+__device__ __forceinline__ void big8_loop(const P& p, char* smem,
+                                          f32x4 (&acc)[GeoOf<P>::NF][GeoOf<P>::MF],
                                           int wave, int lane, int wm, int wn, int m0, int n0,
                                           int nk, bool cont = false, int nm0 = 0, int nn0 = 0,
                                           Pre1 pre1 = {}, Mid mid = {}, Last last = {},
@@ -1893,6 +1945,372 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Persistent 128 x 384 kernel (gemm_p384_kernel): the same 8-phase main loop (big8_*, geometry
+// GeoOf<P384Params>: 8 waves of 64 x 96, 6 x 4 fragments, A m-halves of 8 KiB and W n-halves of
+// 24 KiB per 64 KiB K-tile stage, the same counted waits) for GEMMs whose width is a multiple of
+// 384 and whose 256 x 256 grid quantises badly: D = 384 models (T2T-ViT-14, DeiT-small, Swin
+// stage 3) have out-proj / FC2 at 1.54 tile rounds with the N = 384 -> 512 padding, and the
+// DeiT-base out-proj / FC2 of a strong-scaling shard (64 images: 150 tiles on 256 CUs) leave CUs
+// idle; 128 x 384 tiles need no padding and fill the rounds (launch_t's cost rule picks it).
+// Epilogue straight from the accumulators as the 256 x 256 one (LN fold, bias, GELU, residual
+// LayerNorm, row statistics), rows leaving through a per-wave 3 KiB LDS transpose in four
+// 16-row steps: each row's 96 columns = one whole 128-B line + one 64-B half line.
+// Statistics: one slot per 128-column slab (3 per tile); slab s of the tile is the sum of exactly
+// two waves' partials (wave s, then wave s + 1), the slots past 3 * ntiles written as zero.
+// ---------------------------------------------------------------------------------------------
+constexpr int P3_RAW = 2 * BIG_STAGE;          // raw LN statistics of the tile rows [128][<=8] f32x2
+constexpr int P3_COLRAW = P3_RAW + 8192;       // DMA'd column vectors [3][384] f32
+constexpr int P3_COEF = P3_COLRAW + 4608;      // LayerNorm (mu, r) per tile row [128] f32x2
+constexpr int P3_COLB = P3_COEF + 1024;        // column vectors of the tile being finished [3][384]
+constexpr int P3_PART = P3_COLB + 4608;        // second-wave slab partials [3][128] f32x2
+constexpr int P3_LDS_ALL = P3_PART + 3072;
+constexpr int P3_X = 12;                       // output stores per wave per interior tile
+
+constexpr bool p384_fl(int fl) {
+  return fl == (EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS) ||
+         fl == (EPI_BIAS | EPI_RESID | EPI_STATS) || fl == (EPI_LNIN | EPI_BIAS | EPI_GELU) ||
+         fl == (EPI_LNIN | EPI_BIAS);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc_rows(const void* mat, int64_t ld, int M,
+                                                                int m0, int n0, int rows) {
+  m0 = __builtin_amdgcn_readfirstlane(m0);
+  n0 = __builtin_amdgcn_readfirstlane(n0);
+  const int nr = (min(M - m0, rows) * (int)ld - n0) * 2;
+  return __builtin_amdgcn_make_buffer_rsrc((char*)const_cast<void*>(mat) + ((int64_t)m0 * ld + n0) * 2,
+                                           0, nr, 0x00020000);
+}
+
+template <int FL>
+__device__ __forceinline__ void p3_coop_dma(const GemmParams& p, char* smem, int wave, int lane,
+                                            int m0, int n0) {
+  typedef PersFlags<FL> F;
+  asm volatile("" : "+v"(lane));
+  if constexpr (F::ln) {
+    const float* st = (FL & EPI_LNIN) ? p.stats_in : p.rstats;
+    const int half = p.nslots >> 1;  // 16-B chunks per row
+    const int nch = 128 * half;      // <= 512
+    const int64_t c0 = (int64_t)m0 * half, clast = (int64_t)p.M * half - 1;
+    const int c = wave * 64;
+    if (c < nch) glds16(st + 4 * min(c0 + c + lane, clast), (EVT_LDS char*)smem + P3_RAW + c * 16);
+  }
+  const float* v = nullptr;
+  if (wave == 0 && F::v0) v = p.bias;
+  if (wave == 1 && (FL & EPI_LNIN)) v = p.colsum;
+  if (wave == 1 && (FL & EPI_RESLN)) v = p.rgamma;
+  if (wave == 2 && F::v2) v = p.rbeta;
+  if (v) {  // 384 floats: 96 chunks of 16 B
+    EVT_LDS char* d = (EVT_LDS char*)smem + P3_COLRAW + wave * 1536;
+    glds16(v + min(n0 + 4 * lane, p.N - 4), d);
+    if (lane < 32) glds16(v + min(n0 + 256 + 4 * lane, p.N - 4), d + 1024);
+  }
+}
+
+// Per-row LayerNorm coefficients of the 128 tile rows and a copy of the 3 x 384 column vectors;
+// `tid` in [0, 256) (wave group 1 in the main loop's slot) or [0, 512).
+template <int FL>
+__device__ __forceinline__ void p3_coef(const GemmParams& p, char* smem, int tid, int nthr) {
+  typedef PersFlags<FL> F;
+  asm volatile("" : "+v"(tid));
+  if constexpr (F::ln) {
+    if (tid < 128) {
+      const EVT_LDS f32x2* st = (const EVT_LDS f32x2*)(smem + P3_RAW) + tid * p.nslots;
+      float s1 = 0.f, s2 = 0.f;
+      for (int j = 0; j < p.nslots; ++j) {
+        const f32x2 v = st[j];
+        s1 += v[0];
+        s2 += v[1];
+      }
+      const float mu = s1 * p.inv_d;
+      const float r = rsqrtf(fmaxf(s2 * p.inv_d - mu * mu, 0.f) + p.eps);
+      ((EVT_LDS f32x2*)(smem + P3_COEF))[tid] = f32x2{mu, r};
+    }
+  }
+  const EVT_LDS float* src = (const EVT_LDS float*)(smem + P3_COLRAW);
+  EVT_LDS float* dst = (EVT_LDS float*)(smem + P3_COLB);
+  for (int c = tid; c < 384; c += nthr) {
+    if (F::v0) dst[c] = src[c];
+    if (F::v1) dst[384 + c] = src[384 + c];
+    if (F::v2) dst[768 + c] = src[768 + c];
+  }
+}
+
+template <int FL>
+__device__ __forceinline__ void p3_epilogue(const GemmParams& p, char* smem, f32x4 (&acc)[6][4],
+                                            int wave, int wm, int wn, int m0, int n0, int tn,
+                                            int lane, int spar) {
+  asm volatile("" : "+v"(lane));
+  const int frow = lane & 15, fg = lane >> 4;
+  const EVT_LDS f32x2* coef = (const EVT_LDS f32x2*)(smem + P3_COEF);
+  const EVT_LDS float* colb = (const EVT_LDS float*)(smem + P3_COLB);
+  // 1. MFMA layout: row wm*64 + mt*16 + frow, columns wn*96 + nt*16 + 4 fg + j
+  if constexpr ((FL & EPI_LNIN) != 0) {
+#pragma unroll
+    for (int nt = 0; nt < 6; ++nt) {
+      const int c = wn * 96 + nt * 16 + 4 * fg;
+      const f32x4 b4 = (FL & EPI_BIAS) ? lds4(colb + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 c4 = lds4(colb + 384 + c);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const f32x2 cf = coef[wm * 64 + mt * 16 + frow];
+        const f32x2 nmu = {-cf[0], -cf[0]}, rr = {cf[1], cf[1]};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          f32x2 a = {acc[nt][mt][2 * h], acc[nt][mt][2 * h + 1]};
+          const f32x2 cs = {c4[2 * h], c4[2 * h + 1]}, bb = {b4[2 * h], b4[2 * h + 1]};
+          a = __builtin_elementwise_fma(cs, nmu, a);
+          a = __builtin_elementwise_fma(a, rr, bb);
+          acc[nt][mt][2 * h] = a[0];
+          acc[nt][mt][2 * h + 1] = a[1];
+        }
+      }
+    }
+  } else if constexpr ((FL & EPI_BIAS) != 0) {
+#pragma unroll
+    for (int nt = 0; nt < 6; ++nt) {
+      const int c = wn * 96 + nt * 16 + 4 * fg;
+      f32x4 b4 = lds4(colb + c);
+      if (FL & EPI_RESLN) b4 += lds4(colb + 768 + c);  // + beta of LN(resid)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[nt][mt] += b4;
+    }
+  }
+  if constexpr ((FL & (EPI_GELU | EPI_GELU_ERF)) != 0) {
+#pragma unroll
+    for (int nt = 0; nt < 6; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[nt][mt] = gelu4(acc[nt][mt], (FL & EPI_GELU) ? 0 : 2);
+  }
+  // 2. row pairs (2k, 2k+1): lane row wm*64 + (2k + (fg & 1))*16 + frow, columns
+  //    wn*96 + nt*16 + (fg >> 1)*8 .. + 7
+#pragma unroll
+  for (int nt = 0; nt < 6; ++nt)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) swap_rows16(acc[nt][2 * k], acc[nt][2 * k + 1]);
+  const int rl = wm * 64 + (fg & 1) * 16 + frow;  // + 32 k
+  const int cl = wn * 96 + (fg >> 1) * 8;           // + 16 nt
+  u32x4 rr[2][6];
+  if constexpr ((FL & EPI_RESID) != 0) {
+    const __amdgpu_buffer_rsrc_t rs = tile_rsrc_rows(p.resid, p.ldr, p.M, m0, n0, 128);
+    const int vo = (rl * (int)p.ldr + cl) * 2;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int so = __builtin_amdgcn_readfirstlane(32 * k * (int)p.ldr * 2);
+#pragma unroll
+      for (int nt = 0; nt < 6; ++nt)
+        rr[k][nt] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 32 * nt, so, 0));
+    }
+  }
+  // 3. values (+ residual), bf16 packing and the per-row statistics of the stored values, split
+  //    by 128-column slab: part a = the slab of the wave's first column, part b = the next one
+  const int sa = (wn * 96) >> 7;
+  f32x2 sta[2], stb[2];
+  u32x4 ov[2][6];
+  const bf16x2 one2 = {(bf16)1.0f, (bf16)1.0f};
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    sta[k] = f32x2{0.f, 0.f};
+    stb[k] = f32x2{0.f, 0.f};
+    const f32x2 rc = (FL & EPI_RESLN) ? coef[rl + 32 * k] : f32x2{0.f, 0.f};
+#pragma unroll
+    for (int nt = 0; nt < 6; ++nt) {
+      f32x4 v[2] = {acc[nt][2 * k], acc[nt][2 * k + 1]};
+      if constexpr ((FL & EPI_RESID) != 0) {
+        const int c = cl + 16 * nt;
+        const bf16x8 r8 = __builtin_bit_cast(bf16x8, rr[k][nt]);
+        const f32x2 rrow = {rc[1], rc[1]}, nrm = {-rc[1] * rc[0], -rc[1] * rc[0]};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          f32x4 g = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (FL & EPI_RESLN) g = lds4(colb + 384 + c + 4 * h);
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const f32x2 rv = {(float)r8[4 * h + 2 * q], (float)r8[4 * h + 2 * q + 1]};
+            f32x2 a = {v[h][2 * q], v[h][2 * q + 1]};
+            if (FL & EPI_RESLN) {  // + gamma (r resid - r mu)   (beta already in the bias)
+              const f32x2 t = __builtin_elementwise_fma(rrow, rv, nrm);
+              a = __builtin_elementwise_fma(f32x2{g[2 * q], g[2 * q + 1]}, t, a);
+            } else {
+              a += rv;
+            }
+            v[h][2 * q] = a[0];
+            v[h][2 * q + 1] = a[1];
+          }
+        }
+      }
+      const bf16x8 o = {(bf16)v[0][0], (bf16)v[0][1], (bf16)v[0][2], (bf16)v[0][3],
+                        (bf16)v[1][0], (bf16)v[1][1], (bf16)v[1][2], (bf16)v[1][3]};
+      ov[k][nt] = __builtin_bit_cast(u32x4, o);
+    }
+  }
+  // 4. output: per row pair k and lane-row half h (16 rows), the wave's 16 x 96 block goes through
+  //    its 3 KiB of LDS (the W n-half-1 rows of the next tile's K-tile-1 buffer, not DMA'd before
+  //    that tile's phase 1) and leaves as one whole 128-B line + one 64-B half line per row
+  {
+    EVT_LDS char* scr = (EVT_LDS char*)smem + (spar ^ 1) * BIG_STAGE + Geo<P384Params>::A_TILE +
+                        ((wave & 3) * 96 + 48) * ROWB + (wave >> 2) * 3072;
+    const __amdgpu_buffer_rsrc_t cs = tile_rsrc_rows(p.C, p.ldc, p.M, m0, n0, 128);
+    const int fo = (wn & 1) ? 64 : 0, ho = (wn & 1) ? 0 : 128;  // line / half-line byte offsets
+    const int lrow = lane >> 3, lch = lane & 7, hrow = lane >> 2, hch = lane & 3;
+    const int wcol = wn * 96 * 2;  // the wave's first column, bytes
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if ((fg & 1) == h) {
+#pragma unroll
+          for (int nt = 0; nt < 6; ++nt) {
+            const int ch = 2 * nt + (fg >> 1);
+            *(EVT_LDS u32x4*)(scr + frow * 192 + ch * 16) = ov[k][nt];
+          }
+        }
+        asm volatile("" ::: "memory");  // (a wave's LDS operations execute in order)
+        const int r0 = wm * 64 + 32 * k + 16 * h;
+        const int so = __builtin_amdgcn_readfirstlane(r0 * (int)p.ldc * 2);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {  // whole lines: 8 rows x 128 B per instruction
+          const int r = i * 8 + lrow, ch = (fo >> 4) + lch;
+          const u32x4 v = *(const EVT_LDS u32x4*)(scr + r * 192 + ch * 16);
+          buffer_store_b128<2>(v, cs, r * (int)p.ldc * 2 + wcol + fo + lch * 16, so);
+        }
+        {  // half lines: 16 rows x 64 B
+          const int ch = (ho >> 4) + hch;
+          const u32x4 v = *(const EVT_LDS u32x4*)(scr + hrow * 192 + ch * 16);
+          buffer_store_b128<2>(v, cs, hrow * (int)p.ldc * 2 + wcol + ho + hch * 16, so);
+        }
+        asm volatile("" ::: "memory");
+      }
+  }
+  if constexpr ((FL & EPI_STATS) != 0) {
+    // statistics of the stored values, after the stores (the slab split selects would otherwise
+    // be scheduled between a wide store and its fence)
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int nt = 0; nt < 6; ++nt) {
+        const bool inb = ((wn * 96 + nt * 16) >> 7) != sa;  // wave-uniform
+        const bf16x8 o = __builtin_bit_cast(bf16x8, ov[k][nt]);
+        f32x2 s = {0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          // (from the bf16x8, not bit_cast(bf16x2, ov[k][nt][e]): see pers_epilogue)
+          const bf16x2 w = {o[2 * e], o[2 * e + 1]};
+          s[0] = __builtin_amdgcn_fdot2_f32_bf16(w, one2, s[0], false);
+          s[1] = __builtin_amdgcn_fdot2_f32_bf16(w, w, s[1], false);
+        }
+        if (inb) stb[k] += s;
+        else sta[k] += s;
+      }
+    // lanes fg and fg ^ 2 hold the two 8-column halves of the same row's 16-column groups
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      sta[k][0] += __shfl_xor(sta[k][0], 32, 64);
+      sta[k][1] += __shfl_xor(sta[k][1], 32, 64);
+      stb[k][0] += __shfl_xor(stb[k][0], 32, 64);
+      stb[k][1] += __shfl_xor(stb[k][1], 32, 64);
+    }
+    // slab s = first part (wave s: a for s = 0, b otherwise) + second (wave s + 1, its part a)
+    EVT_LDS f32x2* part = (EVT_LDS f32x2*)(smem + P3_PART);
+    if (wn >= 1 && lane < 32) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) part[(wn - 1) * 128 + wm * 64 + 32 * k + lane] = sta[k];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    big8_bar();
+    if (lane < 32) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int m = m0 + wm * 64 + 32 * k + lane;
+        if (m < p.M) {
+          float* so = p.stats_out + 2 * (int64_t)p.nslots * m;
+          if (wn <= 2) {
+            const f32x2 o = part[wn * 128 + wm * 64 + 32 * k + lane];
+            *(f32x2*)(so + 2 * (3 * tn + wn)) = (wn == 0 ? sta[k] : stb[k]) + o;
+          } else if (tn == p.ntiles - 1) {  // slots past the last tile's slabs: zero
+            for (int s = 3 * p.ntiles; s < p.nslots; ++s) *(f32x2*)(so + 2 * s) = f32x2{0.f, 0.f};
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int FL>
+__device__ __forceinline__ void p3_run(const P384Params& p, int total, int tile, char* smem) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int G = gridDim.x;
+  const int nk = p.K / 64;
+  int tm = tile / p.ntiles, tn = tile - tm * p.ntiles;
+  p3_coop_dma<FL>(p, smem, wave, lane, tm * 128, tn * 384);
+  big8_prologue(p, smem, wave, lane, tm * 128, tn * 384, nk);
+  wait_vmcnt0();  // the first K-tile's waits assume P3_X younger VMEM ops or a drain
+  int par = 0;
+  const bool early = nk >= 3;
+  while (true) {
+    const int m0 = tm * 128, n0 = tn * 384;
+    f32x4 acc[6][4];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int next = tile + G;
+    const bool has_next = next < total;
+    int ntm = 0, ntn = 0;
+    if (has_next) {
+      ntm = next / p.ntiles;
+      ntn = next - ntm * p.ntiles;
+    }
+    const bool cont = has_next && nk >= 2;
+    const int npar = cont ? par ^ (nk & 1) : 0;
+    if (early) {
+      auto pre1 = [&]() { p3_coef<FL>(p, smem, tid - 256, 256); };
+      auto mid = [&]() {
+        if (has_next) p3_coop_dma<FL>(p, smem, wave, lane, ntm * 128, ntn * 384);
+      };
+      big8_loop<P3_X, true, decltype(pre1), decltype(mid), 0, NoOp, 0, NoOp, P384Params>(
+          p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * 128, ntn * 384, pre1, mid, {}, {},
+          par);
+      if (has_next && !cont) big8_prologue(p, smem, wave, lane, ntm * 128, ntn * 384, nk);
+    } else {
+      big8_loop<P3_X, false, NoOp, NoOp, 0, NoOp, 0, NoOp, P384Params>(
+          p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * 128, ntn * 384, {}, {}, {}, {},
+          par);
+      p3_coef<FL>(p, smem, tid, 512);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      big8_bar();
+      if (has_next) {
+        p3_coop_dma<FL>(p, smem, wave, lane, ntm * 128, ntn * 384);
+        if (!cont) big8_prologue(p, smem, wave, lane, ntm * 128, ntn * 384, nk);
+      }
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    p3_epilogue<FL>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, npar);
+    if (!has_next) break;
+    if (m0 + 128 > p.M) wait_vmcnt0();  // edge tile: fewer stores than P3_X issued
+    par = npar;
+    tile = next;
+    tm = ntm;
+    tn = ntn;
+  }
+}
+
+template <int FL>
+__global__ __launch_bounds__(512, 2) void gemm_p384_kernel(GemmParams p, int total) {
+  __shared__ __attribute__((aligned(16))) char smem[P3_LDS_ALL];
+  const int G = gridDim.x;  // XCD-aware order when a multiple of 8
+  const int tile = (G & 7) ? (int)blockIdx.x : (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  if (tile >= total) return;
+  P384Params q;
+  static_cast<GemmParams&>(q) = p;
+  p3_run<FL>(q, total, tile, smem);
+}
+
 // Two dependent GEMMs in one persistent launch: producer FA (out-proj: LN residual, row
 // statistics) over every M panel, then consumer FB (FC1: LN-folded A = the producer's output) in
 // the same tile walk, so the CUs the producer's last, partial tile round
@@ -2153,7 +2571,7 @@ bool gemm_lab_pers_variant(int v) {
 
 bool use_pers(const GemmParams& p, int flags) {
   const int v = g_gemm_variant;
-  if (v != 0 && v != 9 && v != 16 && !gemm_lab_pers_variant(v)) return false;
+  if (v != 0 && v != 9 && v != 16 && v != 31 && !gemm_lab_pers_variant(v)) return false;
   // timeline variants stamp s_memtime through p.pos: never on the patch GEMM (p.pos = the table)
   if ((v == 13 || v == 15) && (flags & EPI_POS)) return false;
   if (p.N % 8 || p.vec_ok < 2) return false;
@@ -2205,6 +2623,36 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 0, false>), dim3(G), dim3(512), 0, s, q, total);
   else
     hipLaunchKernelGGL((gemm_pers_kernel<FL>), dim3(G), dim3(512), 0, s, q, total);
+  return hipGetLastError();
+}
+
+// 128 x 384 persistent tiles (gemm_p384_kernel) where the width is a multiple of 384 and their
+// tile rounds cost less than the 256 x 256 grid's: rounds x tile work, a 128 x 384 tile = 0.75 of
+// a 256 x 256 one (e.g. T2T-ViT-14 out-proj / FC2: 2 x 0.75 against 2 rounds of half-padded
+// tiles; DeiT-base out-proj / FC2 at 64 images: 1 x 0.75 against one round on 150 CUs).
+// evt_set_gemm_variant 30 forces it wherever it applies, 31 never.
+bool use_p384(const GemmParams& p, int flags) {
+  const int v = g_gemm_variant;
+  if ((v != 0 && v != 30) || p.N % 384 || p.vec_ok < 2 || p.K < 64) return false;
+  if ((flags & (EPI_LNIN | EPI_RESLN)) && (p.nslots > 8 || p.nslots % 2 || p.stats_step > 1))
+    return false;
+  if ((flags & EPI_STATS) && 3 * (p.N / 384) > p.nslots) return false;
+  if (v == 30) return true;
+  const int G = num_cus();
+  const int64_t t0 = (int64_t)((p.M + 255) / 256) * ((p.ntiles * GEMM_BN + 255) / 256);
+  const int64_t t1 = (int64_t)((p.M + 127) / 128) * (p.N / 384);
+  const double c0 = (double)((t0 + G - 1) / G), c1 = 0.75 * (double)((t1 + G - 1) / G);
+  return c1 < 0.9 * c0;
+}
+
+template <int FL>
+hipError_t launch_p384(const GemmParams& p, hipStream_t s) {
+  GemmParams q = p;
+  q.ntiles = p.N / 384;
+  const int total = ((p.M + 127) / 128) * q.ntiles;
+  int G = min(total, num_cus());
+  if (G >= 8) G &= ~7;
+  hipLaunchKernelGGL((gemm_p384_kernel<FL>), dim3(G), dim3(512), 0, s, q, total);
   return hipGetLastError();
 }
 
@@ -2268,6 +2716,9 @@ hipError_t launch_t(const GemmParams& p, hipStream_t s) {
     return hipErrorNotSupported;
   } else {
     if constexpr (std::is_same<T, bf16>::value) {
+      if constexpr (p384_fl(FL)) {
+        if (use_p384(p, FL)) return launch_p384<FL>(p, s);
+      }
       if (use_big(p, FL)) {
         if constexpr (pers_fl(FL)) {
           if (use_pers(p, FL)) return use_sk(p) ? launch_sk<FL>(p, s) : launch_pers<FL>(p, s);
@@ -2408,7 +2859,7 @@ __global__ void fold_kernel(const T* __restrict__ Wp, int Kpad, const float* __r
 int device_cus() { return num_cus(); }
 void gemm_set_variant(int v) { g_gemm_variant = v; }
 bool gemm_variant_supported(int v) {
-  return v == 0 || v == 1 || v == 2 || v == 6 || v == 8 || v == 9 || v == 16 ||
+  return v == 0 || v == 1 || v == 2 || v == 6 || v == 8 || v == 9 || v == 16 || v == 30 || v == 31 ||
          gemm_lab_pers_variant(v)
 #ifdef EVT_GEMM_LAB
          || v == 106 || v == 108
@@ -2428,8 +2879,11 @@ hipError_t gemm_chain_launch(int dtype, int fa, const GemmParams& pa, int fb, co
                              const ChainWords& cw, hipStream_t s) {
   constexpr int RES = EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS;
   if (dtype != DT_BF16 || g_gemm_variant != 0 || fa != RES || !cw.sync) return hipErrorNotSupported;
+  // only where both GEMMs would take the 256 x 256 persistent kernel on their own (bitwise the
+  // separate launches)
   if (pa.M != pb.M || pa.N % BIG_BN || pb.N % BIG_BN || pa.K / 64 < 3 || pb.K / 64 < 3 ||
-      !use_pers(pa, fa) || !use_pers(pb, fb))
+      !use_big(pa, fa) || !use_big(pb, fb) || !use_pers(pa, fa) || !use_pers(pb, fb) ||
+      use_p384(pa, fa) || use_p384(pb, fb))
     return hipErrorNotSupported;
   if (fb == (EPI_LNIN | EPI_BIAS | EPI_GELU))
     return launch_chain<RES, EPI_LNIN | EPI_BIAS | EPI_GELU>(pa, pb, cw, s);

@@ -463,7 +463,8 @@ int evt_attention_mx8(const void* qkv, int64_t ldq, void* q8, int64_t ldq8, uint
  * 0 = automatic (256x256 tiles when the problem has >= 256 of them, the tile-persistent kernel
  * for the fused epilogues, else 128x128), 1 = always 128x128, 2 / 6 / 8 = non-persistent 256x256
  * tiles with the plain / interleaved / 8-phase ping-pong main loop whenever the packed width
- * allows, 9 = tile-persistent, 16 = stream-K persistent where it applies. Builds with
+ * allows, 9 = tile-persistent, 16 = stream-K persistent where it applies, 30 = the 128 x 384
+ * persistent tiles wherever the width allows (multiple of 384), 31 = automatic without them. Builds with
  * EVT_LAB=1 (-DEVT_GEMM_LAB) also accept the ablation / timeline variants 10, 11, 13, 15, 17-25,
  * 106, 108; other values return EVT_EINVAL. */
 int evt_set_gemm_variant(int variant);

@@ -1,4 +1,4 @@
-"""Experiment: the bs=512 DeiT-base batch as S concurrent sub-batches on S HIP streams (one model
+"""Experiment: the bs=512 (argv[2]) DeiT-base batch as S concurrent sub-batches on S HIP streams (one model
 handle each), so that one sub-batch's GEMM tails / memory-bound kernels overlap another's work.
 Interleaved rounds in one process; images/s per configuration."""
 import sys
@@ -9,7 +9,7 @@ import torch
 sys.path.insert(0, ".")
 from edgevisiontransformer_amd.modeling.models import vit as mod  # noqa: E402
 
-B = 512
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 512
 g = torch.Generator(device="cuda").manual_seed(1)
 img = torch.randn((B, 3, 224, 224), generator=g, device="cuda")
 logits = torch.empty((B, 1000), device="cuda")

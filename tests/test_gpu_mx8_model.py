@@ -24,7 +24,13 @@ pytestmark = pytest.mark.gpu
 MX8_COS, MX8_REL = 0.98, 0.25
 
 
-@pytest.mark.parametrize("name", list(CASES))
+# EVT_DTYPE_MX8 is built for head size 64 and widths that are multiples of 64 (include/evt.h); the
+# other head sizes run in bf16 / fp32 (tests/test_gpu_model.py)
+MX8_CASES = [n for n in CASES if CASES[n][0]["dim"] % 64 == 0
+             and CASES[n][0]["dim"] // CASES[n][0]["heads"] == 64]
+
+
+@pytest.mark.parametrize("name", MX8_CASES)
 def test_golden_mx8(gpu, name):
     m, img = _model_for(name, "mx8", gpu)
     z = np.load(os.path.join(GOLDEN, f"{name}.npz"))

@@ -287,7 +287,7 @@ def _stats32(xq):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f32"])
-@pytest.mark.parametrize("variant", [1, 2, 8, 9, 10, 0])
+@pytest.mark.parametrize("variant", [1, 2, 8, 9, 10, 0, 30, 31])
 @pytest.mark.parametrize("M,D,N,gelu", [(300, 768, 2304, False), (600, 384, 1536, True),
                                         (197, 192, 537, True), (2900, 768, 3072, True)])
 def test_dense_layernorm_folded_input(gpu, dtype, variant, M, D, N, gelu):
@@ -319,9 +319,10 @@ def test_dense_layernorm_folded_input(gpu, dtype, variant, M, D, N, gelu):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f32"])
-@pytest.mark.parametrize("variant", [1, 2, 8, 9, 10, 0])
+@pytest.mark.parametrize("variant", [1, 2, 8, 9, 10, 0, 30, 31])
 @pytest.mark.parametrize("M,K,D", [(300, 768, 768), (513, 3072, 384), (197, 576, 192),
-                                   (2900, 768, 768)])
+                                   (2900, 768, 768), (12608, 3072, 768), (1, 384, 384),
+                                   (129, 1152, 384), (50432, 384, 384)])
 def test_dense_layernorm_residual_and_stats(gpu, dtype, variant, M, K, D):
     """out-proj / FC2 as run in the model: + bias + LN(resid) residual (the reference's quirk:
     the residual is the normalised input), storing the new stream and its row statistics."""
@@ -352,3 +353,78 @@ def test_dense_layernorm_residual_and_stats(gpu, dtype, variant, M, K, D):
     # statistics are of the values as stored
     torch.testing.assert_close(stats_out.double().cpu().sum(1), _stats32(got).double().sum(1),
                                rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("M,K,N", [(513, 384, 384), (3000, 1536, 384), (12608, 768, 768), (1, 128, 1152)])
+@pytest.mark.parametrize("variant", [30, 0])
+def test_dense_residual_plain_stats(gpu, M, K, N, variant):
+    """The Swin proj / FC2 form (BIAS|RESID|STATS: x + f(LN(x)) with the plain residual) on the
+    128 x 384 persistent tiles (variant 30) and the automatic choice: values and the row
+    statistics of the stored values (every slot written, the slots past 3 * N / 384 zero)."""
+    A64, W64, b64 = _rand((M, K), 61), _rand((K, N), 62, 1 / math.sqrt(K)), _rand((N,), 63, 0.1)
+    R64 = _rand((M, N), 64)
+    Aq, Rq = _q(A64, "bf16"), _q(R64, "bf16")
+    wp, kpad, npad = _ops.pack(W64.float().to(gpu), "bf16")
+    bias = torch.zeros(npad, device=gpu)
+    bias[:N] = b64.float().to(gpu)
+    st = torch.full((M, _nslots(N), 2), float("nan"), device=gpu)
+    lib = _lib.load_library()
+    lib.evt_set_gemm_variant(variant)
+    try:
+        C = _ops.dense("bf16", _lib.EPI_BIAS | _lib.EPI_RESID | _lib.EPI_STATS,
+                       Aq.to(torch.bfloat16).to(gpu), wp, kpad, npad, M, N, bias=bias,
+                       resid=Rq.to(torch.bfloat16).to(gpu), stats_out=st, ln_width=N)
+        torch.cuda.synchronize()
+    finally:
+        lib.evt_set_gemm_variant(0)
+    ref = Aq @ _q(W64.float().double(), "bf16") + b64.float().double() + Rq
+    got = C.double().cpu()
+    torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(st.double().cpu().sum(1), _stats32(got).double().sum(1),
+                               rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("flags", ["resln", "lnin_gelu"])
+def test_dense_p384_rows_independent_of_position(gpu, flags):
+    """128 x 384 tiles: a row's outputs (and statistics) are the same bits wherever it sits in the
+    batch (tile offsets, neighbours, last partial panel): the product contract's batch-position
+    independence for a fixed kernel selection."""
+    M, K, N, shift = 1000, 768, 768, 37
+    A64 = _rand((M + shift, K), 71)
+    W64, b64 = _rand((K, N), 72, 1 / math.sqrt(K)), _rand((N,), 73, 0.1)
+    x64 = _rand((M + shift, N), 74)
+    g64, be64 = 1.0 + _rand((N,), 75, 0.1), _rand((N,), 76, 0.1)
+    lib = _lib.load_library()
+    outs = []
+    lib.evt_set_gemm_variant(30)
+    try:
+        for off in (0, shift):
+            Aq = _q(A64[off:off + M], "bf16").to(torch.bfloat16).to(gpu)
+            xq = _q(x64[off:off + M], "bf16")
+            if flags == "resln":
+                wp, kpad, npad = _ops.pack(W64.float().to(gpu), "bf16")
+                bias = torch.zeros(npad, device=gpu)
+                bias[:N] = b64.float().to(gpu)
+                st = torch.full((M, _nslots(N), 2), float("nan"), device=gpu)
+                C = _ops.dense("bf16", _lib.EPI_BIAS | _lib.EPI_RESID | _lib.EPI_RESLN | _lib.EPI_STATS,
+                               Aq, wp, kpad, npad, M, N, bias=bias,
+                               resid=xq.to(torch.bfloat16).to(gpu), rstats=_stats32(xq).to(gpu),
+                               rgamma=g64.float().to(gpu), rbeta=be64.float().to(gpu),
+                               stats_out=st, ln_width=N)
+            else:
+                g = g64.float().to(gpu)
+                wp, kpad, npad = _ops.pack(W64.float().to(gpu), "bf16", row_scale=g)
+                colsum, cvec = _ops.ln_fold("bf16", wp, kpad, npad, W64.float().to(gpu),
+                                            be64.float().to(gpu), b64.float().to(gpu))
+                C = _ops.dense("bf16", _lib.EPI_LNIN | _lib.EPI_BIAS | _lib.EPI_GELU,
+                               xq.to(torch.bfloat16).to(gpu), wp, kpad, npad, M, N, bias=cvec,
+                               colsum=colsum, stats_in=_stats32(xq).to(gpu), ln_width=N)
+                st = None
+            torch.cuda.synchronize()
+            outs.append((C.cpu(), None if st is None else st.cpu()))
+    finally:
+        lib.evt_set_gemm_variant(0)
+    (c0, s0), (c1, s1) = outs
+    assert torch.equal(c0[shift:], c1[:M - shift])
+    if s0 is not None:
+        assert torch.equal(s0[shift:], s1[:M - shift])
