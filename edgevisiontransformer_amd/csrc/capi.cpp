@@ -1511,7 +1511,7 @@ int evt_swin_forward(evt_model* m, const float* img, int B, float* logits, void*
       }
     }
     for (const SwinBlock& bl : st.blocks) {
-      const bool fuse96 = dt == DT_BF16 && C == 96 && st.H == 3 && gemm_variant() == 0;
+      const bool fuse96 = dt == DT_BF16 && C == 96 && st.H == 3 && gemm_auto();
       const double slot_rows = (double)rows * stats_slots(C) * 8;
       if (fuse96) {  // stage-1 attention sublayer fused (swin.hip, swin_attn96_kernel)
         ProfScope ps(m, EVT_PROF_ATTN_SUBLAYER, s);
@@ -1545,7 +1545,7 @@ int evt_swin_forward(evt_model* m, const float* img, int B, float* logits, void*
         pc.resid = m->x; pc.ldr = Cst; pc.stats_out = m->sm; pc.ln_width = C;
         EVT_RC(dense(m, bl.proj, pc, s));
       }
-      if (dt == DT_BF16 && C == 96 && st.mlp == 384 && gemm_variant() == 0) {
+      if (dt == DT_BF16 && C == 96 && st.mlp == 384 && gemm_auto()) {
         // stage-1 MLP (C = 96) fused: hidden kept on chip (swin.hip, swin_mlp96_kernel)
         ProfScope ps(m, EVT_PROF_MLP, s);
         prof_work(m, 4.0 * rows * C * st.mlp, 2.0 * rows * C * es + 2 * slot_rows +

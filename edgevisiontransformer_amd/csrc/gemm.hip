@@ -674,24 +674,31 @@ __device__ __forceinline__ void big8_stage(const P& p, char* smem, int wave, int
   const int srow = lane >> 3, sslot = lane & 7;
   EVT_LDS char* base = (EVT_LDS char*)smem + ((T ^ par) & 1) * BIG_STAGE;
   const int64_t koff = (int64_t)T * ROWB + ((sslot ^ srow) << 4);
-  if constexpr (Gm::BM != 256) {  // general geometry: 8-row groups g of the region, in order
-    if (j == 0 || j == 3) {  // A m-half (j == 3): rows wm * WR + half * WR / 2 + [0, WR / 2)
-#pragma unroll
-      for (int i = 0; i < Gm::AI; ++i) {
-        const int g = wave * Gm::AI + i, gpw = Gm::WR / 16;  // groups per wave-row half
-        const int row = (g / gpw) * Gm::WR + (j == 3 ? Gm::WR / 2 : 0) + (g % gpw) * 8;
-        const int gm = min(m0 + row + srow, p.M - 1);
-        glds16((const char*)p.A + (int64_t)gm * (p.lda * 2) + koff, base + row * ROWB);
-      }
-    } else {  // W n-half (j == 2): rows wn * WC + half * WC / 2 + [0, WC / 2)
-#pragma unroll
-      for (int i = 0; i < Gm::WI; ++i) {
-        const int g = wave * Gm::WI + i, gpw = Gm::WC / 16;
-        const int row = (g / gpw) * Gm::WC + (j == 2 ? Gm::WC / 2 : 0) + (g % gpw) * 8;
-        glds16((const char*)p.W + (int64_t)(n0 + row + srow) * (p.ldw * 2) + koff,
-               base + Gm::A_TILE + row * ROWB);
-      }
-    }
+  if constexpr (Gm::BM != 256) {
+    // general geometry: a K-tile's 8 DMA instructions per wave in the region order of the 256 x 256
+    // one (A m-half 0, W n-half 0, W n-half 1, A m-half 1: AI, WI, WI, AI instructions), issued
+    // two per phase: "j" is the pair (0, 1: the first half of that order, 2, 3: the second), so
+    // unequal regions (1 + 3 + 3 + 1 for 128 x 384) still spread evenly over the phases
+    auto a_ins = [&](int h, int i) {  // A m-half h, instruction i of AI: rows wm*WR + h*WR/2 + ..
+      const int g = wave * Gm::AI + i, gpw = Gm::WR / 16;
+      const int row = (g / gpw) * Gm::WR + h * (Gm::WR / 2) + (g % gpw) * 8;
+      const int gm = min(m0 + row + srow, p.M - 1);
+      glds16((const char*)p.A + (int64_t)gm * (p.lda * 2) + koff, base + row * ROWB);
+    };
+    auto w_ins = [&](int h, int i) {  // W n-half h, instruction i of WI: rows wn*WC + h*WC/2 + ..
+      const int g = wave * Gm::WI + i, gpw = Gm::WC / 16;
+      const int row = (g / gpw) * Gm::WC + h * (Gm::WC / 2) + (g % gpw) * 8;
+      glds16((const char*)p.W + (int64_t)(n0 + row + srow) * (p.ldw * 2) + koff,
+             base + Gm::A_TILE + row * ROWB);
+    };
+    auto ins = [&](int q) {  // instruction q (0..7) of the K-tile's sequence
+      if (q < Gm::AI) a_ins(0, q);
+      else if (q < Gm::AI + Gm::WI) w_ins(0, q - Gm::AI);
+      else if (q < Gm::AI + 2 * Gm::WI) w_ins(1, q - Gm::AI - Gm::WI);
+      else a_ins(1, q - Gm::AI - 2 * Gm::WI);
+    };
+    ins(2 * j);
+    ins(2 * j + 1);
     return;
   }
 #pragma unroll
@@ -801,17 +808,23 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem,
     reads();
     dmas();
 #endif
-    // retire what the next phase reads (phases 4, 1, 2 precede reading phases)
+    // retire what the next phase reads (phases 4, 1, 2 precede reading phases). W0: after phase 0
+    // the W n-half-1 region must have landed; its last instruction is followed by 8 younger ones
+    // in the 256 x 256 order, by 7 in the paired order of the 128 x 384 geometry (big8_stage)
+    constexpr int W0 = Gm::WI == 3 ? 7 : 8;
     if (ph != 2) {
       if (MODE == 0) {
         if (ph == 3 && X3 > 0 && x3on) wait_vm<8 + X + X3>();
+        else if (ph == 0) wait_vm<W0 + X>();
         else wait_vm<8 + X>();
       }
       else if (cont) {  // the steady-state DMA pattern continues: steady-state waits
         if (ph == 3) wait_vm<8 + X + X3>();
+        else if (ph == 0) wait_vm<W0 + X>();
         else wait_vm<8 + X>();
       } else if (MODE == 1) {
         if (ph == 3) wait_vm<4 + X>();
+        else if (ph == 0) wait_vm<W0 + X>();
         else wait_vm<8 + X>();
       } else if (ph == 0) {
         wait_vm<Gm::AI + X>();  // the last K-tile's A m-half-1 region (j3) follows
