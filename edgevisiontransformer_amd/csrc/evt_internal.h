@@ -261,7 +261,10 @@ struct SwinEmbedParams {
 hipError_t swin_embed96_launch(const SwinEmbedParams& p, hipStream_t s);
 int gemm_variant();  // the calling thread's evt_set_gemm_variant value (0 = automatic)
 // automatic kernel selection (0; 30 / 31 only steer the 128 x 384 tiles): fused kernels allowed
-inline bool gemm_auto() { const int v = gemm_variant(); return v == 0 || v == 30 || v == 31; }
+inline bool gemm_auto() {
+  const int v = gemm_variant();
+  return v == 0 || v == 30 || v == 31 || v == 32;
+}
 bool gemm_variant_supported(int v);  // compiled into this build (lab variants: EVT_GEMM_LAB)
 
 // ---- MXFP8 (mx8.hip): e4m3fn elements, e8m0 scale per 32 K, scales S[K/128][ld] dwords ----

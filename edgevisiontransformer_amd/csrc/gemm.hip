@@ -494,7 +494,8 @@ constexpr int BIG_STAGE = 2 * BIG_TILE;       // 64 KiB per K-tile
 
 // evt_set_gemm_variant, per calling thread (launch decisions are made on the launching thread):
 // 0 auto, 1 force 128x128, 2 / 6 / 8 non-persistent 256x256 main loops, 9 tile-persistent,
-// 16 stream-K, 30 128 x 384 persistent wherever it applies, 31 automatic without it. Lab builds (-DEVT_GEMM_LAB) add the ablation / timeline / A-B variants 10, 11, 13,
+// 16 stream-K, 30 128 x 384 persistent wherever it applies, 31 automatic without it, 32 automatic
+// with the round-3 tile rule (256x256 only from 256 tiles up). Lab builds (-DEVT_GEMM_LAB) add the ablation / timeline / A-B variants 10, 11, 13,
 // 15, 17-25, 106, 108 used by scripts/gemm_bench.py and scripts/probe/pers_timeline.py.
 thread_local int g_gemm_variant = 0;
 // Lab A/B: -DEVT_EPI_PACK_FIRST=0 (persistent epilogue without residual: swap fp32 rows, then pack)
@@ -502,14 +503,24 @@ thread_local int g_gemm_variant = 0;
 #define EVT_EPI_PACK_FIRST 1
 #endif
 
+int num_cus();
+
 bool use_big(const GemmParams& p, int flags) {
   if ((p.ntiles * GEMM_BN) % BIG_BN) return false;
   if (!(flags & EPI_OUT_F32) && p.vec_ok < 2) return false;  // big epilogue: 16-B bf16 stores only
-  const int v = g_gemm_variant == 31 ? 0 : g_gemm_variant;  // 31: automatic without 128 x 384
+  // 31: automatic without 128 x 384; 32: automatic with the round-3 rule (>= 256 big tiles)
+  const int v = (g_gemm_variant == 31 || g_gemm_variant == 32) ? 0 : g_gemm_variant;
   if (v == 1) return false;
   if (v >= 2) return true;
-  // enough 256x256 tiles to fill the chip at least once
-  return (int64_t)((p.M + 255) / 256) * (p.ntiles * GEMM_BN / 256) >= 256;
+  // 256x256 tiles unless their rounds cost more: time in 256-tile units, the 128x128 kernel at a
+  // quarter of the work per tile and about half the FLOP rate (measured at 64 images: FC2 107 us
+  // on 594 128x128 tiles against ~80 us for one round of 150 256x256 tiles); tiny problems (the
+  // bs1 forward) keep the small tiles
+  const int64_t G = num_cus();
+  const int64_t t256 = (int64_t)((p.M + 255) / 256) * (p.ntiles * GEMM_BN / 256);
+  const int64_t t128 = (int64_t)((p.M + 127) / 128) * p.ntiles;
+  if (g_gemm_variant == 32) return t256 >= 256;
+  return (t256 + G - 1) / G <= 0.5 * (double)((t128 + G - 1) / G);
 }
 
 // Epilogue of the 256x256 kernels: two passes staged through the (idle) 128 KiB of LDS; in
@@ -2584,7 +2595,7 @@ bool gemm_lab_pers_variant(int v) {
 
 bool use_pers(const GemmParams& p, int flags) {
   const int v = g_gemm_variant;
-  if (v != 0 && v != 9 && v != 16 && v != 31 && !gemm_lab_pers_variant(v)) return false;
+  if (v != 0 && v != 9 && v != 16 && v != 31 && v != 32 && !gemm_lab_pers_variant(v)) return false;
   // timeline variants stamp s_memtime through p.pos: never on the patch GEMM (p.pos = the table)
   if ((v == 13 || v == 15) && (flags & EPI_POS)) return false;
   if (p.N % 8 || p.vec_ok < 2) return false;
@@ -2602,7 +2613,7 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
   q.ntiles = (p.ntiles * GEMM_BN) / BIG_BN;
   const int total = ((p.M + BIG_BM - 1) / BIG_BM) * q.ntiles;
   int G = min(total, g_gemm_variant == 10 ? 8 : g_num_cus);  // 10: few blocks, many tiles each
-  if (G >= 8) G &= ~7;
+  if (G >= 8 && total > G) G &= ~7;  // (one round: one block per tile, no rounding down)
   if (false) {
   }
 #ifdef EVT_GEMM_LAB
@@ -2650,12 +2661,12 @@ bool use_p384(const GemmParams& p, int flags) {
   if ((flags & (EPI_LNIN | EPI_RESLN)) && (p.nslots > 8 || p.nslots % 2 || p.stats_step > 1))
     return false;
   if ((flags & EPI_STATS) && 3 * (p.N / 384) > p.nslots) return false;
-  if (v == 30) return true;
-  const int G = num_cus();
-  const int64_t t0 = (int64_t)((p.M + 255) / 256) * ((p.ntiles * GEMM_BN + 255) / 256);
-  const int64_t t1 = (int64_t)((p.M + 127) / 128) * (p.N / 384);
-  const double c0 = (double)((t0 + G - 1) / G), c1 = 0.75 * (double)((t1 + G - 1) / G);
-  return c1 < 0.9 * c0;
+  // automatic selection: never. Measured (round 4, rocprofv3, same box): a 128 x 384 tile takes
+  // as long per K-tile as a 256 x 256 one (the main loop is bound by its 8 LDS-DMA instructions
+  // per wave per K-tile, the same for both shapes, not by its MFMAs), so 0.75 of the work runs at
+  // 0.75 of the FLOP rate: T2T-ViT-14 out-proj / FC2 53.1 vs 52.8 us, Swin-T 65.2 vs 65.1 us,
+  // DeiT-base at 64 images 80.8 vs 70.6 us (128x128). Kept as the forced diagnostic variant 30.
+  return v == 30;
 }
 
 template <int FL>
@@ -2664,7 +2675,7 @@ hipError_t launch_p384(const GemmParams& p, hipStream_t s) {
   q.ntiles = p.N / 384;
   const int total = ((p.M + 127) / 128) * q.ntiles;
   int G = min(total, num_cus());
-  if (G >= 8) G &= ~7;
+  if (G >= 8 && total > G) G &= ~7;
   hipLaunchKernelGGL((gemm_p384_kernel<FL>), dim3(G), dim3(512), 0, s, q, total);
   return hipGetLastError();
 }
@@ -2873,6 +2884,7 @@ int device_cus() { return num_cus(); }
 void gemm_set_variant(int v) { g_gemm_variant = v; }
 bool gemm_variant_supported(int v) {
   return v == 0 || v == 1 || v == 2 || v == 6 || v == 8 || v == 9 || v == 16 || v == 30 || v == 31 ||
+         v == 32 ||
          gemm_lab_pers_variant(v)
 #ifdef EVT_GEMM_LAB
          || v == 106 || v == 108
