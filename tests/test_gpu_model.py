@@ -67,14 +67,27 @@ def test_golden_bf16(gpu, name):
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 def test_batch_independence(gpu, dtype):
-    """Images are independent (reference has no cross-image op): a 37-image batch must equal the
-    per-image results, bit for bit, and batch sizes past the first build must re-plan."""
+    """Images are independent (reference has no cross-image op): for a fixed GEMM kernel selection a
+    37-image batch equals the per-image results bit for bit (batch sizes past the first build
+    re-plan), and at 37 images under the automatic selection (which may pick 256 x 256 tiles for
+    the batch and 128 x 128 for one image) the rows follow their images through a roll of the
+    batch bit for bit."""
+    from edgevisiontransformer_amd import _lib
     m = get_deit_tiny(dtype=dtype, seed=3, device=gpu)
     img = torch.from_numpy(make_images(37, seed=9)).to(gpu)
-    full = m(img)
-    parts = torch.cat([m(img[i:i + 1]) for i in (0, 17, 36)])
-    torch.cuda.synchronize()
+    lib = _lib.load_library()
+    lib.evt_set_gemm_variant(1)  # every GEMM on the 128 x 128 kernel, whatever the batch
+    try:
+        full = m(img)
+        parts = torch.cat([m(img[i:i + 1]) for i in (0, 17, 36)])
+        torch.cuda.synchronize()
+    finally:
+        lib.evt_set_gemm_variant(0)
     assert torch.equal(full[[0, 17, 36]], parts)
+    auto = m(img)
+    rolled = m(torch.roll(img, 11, 0))
+    torch.cuda.synchronize()
+    assert torch.equal(torch.roll(auto, 11, 0), rolled)
 
 
 def test_deit_small_bf16_vs_oracle(gpu):
