@@ -509,7 +509,8 @@ bool use_big(const GemmParams& p, int flags) {
   if ((p.ntiles * GEMM_BN) % BIG_BN) return false;
   if (!(flags & EPI_OUT_F32) && p.vec_ok < 2) return false;  // big epilogue: 16-B bf16 stores only
   // 31: automatic without 128 x 384; 32: automatic with the round-3 rule (>= 256 big tiles)
-  const int v = (g_gemm_variant == 31 || g_gemm_variant == 32) ? 0 : g_gemm_variant;
+  const int v = (g_gemm_variant == 31 || g_gemm_variant == 32 || g_gemm_variant == 33)
+                    ? 0 : g_gemm_variant;
   if (v == 1) return false;
   if (v >= 2) return true;
   // 256x256 tiles unless their rounds cost more: time in 256-tile units, the 128x128 kernel at a
@@ -602,6 +603,17 @@ struct NoOp {
 #ifndef EVT_RES_PF
 #define EVT_RES_PF 0
 #endif
+// 256 x 256 geometry: phase 3 of each K-tile but the last reads the NEXT K-tile's W n-half-0
+// fragments into the registers B n-half 1 leaves free (1), so that phase 0 reads 8 fragments
+// instead of 12 (the ping-pong partner's MFMA block covers 4 / 8 / 8 / 4 reads per phase instead
+// of 12 / 4 / 8 / 0); the regions of a K-tile are then DMA'd W n-half 0 first (j = 0 <-> 1), so
+// that region keeps four phases of flight time before the phase-2 wait that retires it. 0: the
+// product schedule (measured round 4, lab EVT_LAB_DEFS=-DEVT_BPF=1 against it in 3 alternating
+// same-box pairs: DeiT-base 28.35k vs 28.64k img/s, QKV / FC1 unchanged, out-proj / FC2 +6 / +9 us
+// from the spills it causes: phase 0's fragment reads do not bound the loop)
+#ifndef EVT_BPF
+#define EVT_BPF 0
+#endif
 
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -676,6 +688,26 @@ __device__ __forceinline__ const char* gather_addr(const GemmParams& p, int gm, 
   return (const char*)p.A + (src * p.lda + c) * 2;
 }
 
+// 256 x 256 plain loaders: the DMA pieces are buffer_load ... lds through a per-tile descriptor
+// (SGPR base at the panel's first row, rows past M read zeros) with a tile-invariant 32-bit lane
+// offset and the K-tile offset in soffset (1), instead of global_load_lds on a 64-bit address
+// formed per piece (0: ~8 VALU per piece, 64 per K-tile per wave, in the issue slots beside the
+// partner wave's MFMAs)
+#ifndef EVT_BDMA
+#define EVT_BDMA 1
+#endif
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t dma_rsrc(const void* mat, int64_t ld, int rows,
+                                                          int r0) {
+  r0 = __builtin_amdgcn_readfirstlane(r0);
+  rows = __builtin_amdgcn_readfirstlane(rows);
+  return __builtin_amdgcn_make_buffer_rsrc((char*)const_cast<void*>(mat) + (int64_t)r0 * ld * 2, 0,
+                                           max(0, min(rows - r0, 256)) * (int)ld * 2, 0x00020000);
+}
+__device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, int voff, int soff,
+                                       EVT_LDS void* lds_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, lds_base, 16, voff, soff, 0, 0);
+}
+
 // DMA region j of K-tile T into buffer (T ^ par) & 1 (par: the buffer parity of the tile's
 // K-tile 0; persistent kernel with an odd K-tile count: alternates from tile to tile).
 template <typename P>
@@ -712,6 +744,7 @@ __device__ __forceinline__ void big8_stage(const P& p, char* smem, int wave, int
     ins(2 * j + 1);
     return;
   }
+  if (EVT_BPF) j = j < 2 ? 1 - j : j;  // DMA order W n-half 0, A m-half 0, W n-half 1, A m-half 1
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int r = (wave * 2 + i) * 8;  // region row of this wave-instruction (8 rows)
@@ -722,12 +755,25 @@ __device__ __forceinline__ void big8_stage(const P& p, char* smem, int wave, int
         glds16(gather_addr<1>(p, gm, T * 64 + ((sslot ^ srow) << 3)), base + row * ROWB);
       else if constexpr (std::is_same<P, UnfoldParams>::value)
         glds16(gather_addr<2>(p, gm, T * 64 + ((sslot ^ srow) << 3)), base + row * ROWB);
+      else if (EVT_BDMA)  // one lane offset per wave (instruction i, region j: + 8 i, + 64 rows)
+        bdma16(dma_rsrc(p.A, p.lda, p.M, m0),
+               (((wave * 16) & 63) + (((wave * 16) >> 6) << 7) + srow) * ((int)p.lda * 2) +
+                   ((sslot ^ srow) << 4),
+               __builtin_amdgcn_readfirstlane(T * ROWB + (8 * i + (j == 3 ? 64 : 0)) * (int)p.lda * 2),
+               base + row * ROWB);
       else
         glds16((const char*)p.A + (int64_t)gm * (p.lda * 2) + koff, base + row * ROWB);
     } else {
       const int row = ((r >> 5) << 6) + (r & 31) + (j == 2 ? 32 : 0);
-      glds16((const char*)p.W + (int64_t)(n0 + row + srow) * (p.ldw * 2) + koff,
-             base + BIG_TILE + row * ROWB);
+      if (EVT_BDMA)  // (the packed weight has its rows padded to the 256-wide tiles)
+        bdma16(dma_rsrc(p.W, p.ldw, n0 + 256, n0),
+               ((((wave * 16) >> 5) << 6) + ((wave * 16) & 31) + srow) * ((int)p.ldw * 2) +
+                   ((sslot ^ srow) << 4),
+               __builtin_amdgcn_readfirstlane(T * ROWB + (8 * i + (j == 2 ? 32 : 0)) * (int)p.ldw * 2),
+               base + BIG_TILE + row * ROWB);
+      else
+        glds16((const char*)p.W + (int64_t)(n0 + row + srow) * (p.ldw * 2) + koff,
+               base + BIG_TILE + row * ROWB);
     }
   }
 }
@@ -756,16 +802,55 @@ __device__ __forceinline__ void big8_prologue(const P& p, char* smem, int wave, 
 // final MFMA phase and group 0 the resync barrier after the loop, so group 0 starts its epilogue
 // while group 1 still issues its last 16 MFMAs (the two barriers cancel in every wave's count).
 // ph3: issues X3 further VMEM loads at the start of phase 3 (added to that phase's wait).
-template <int MODE, int X, bool OPEN = false, int X3 = 0, typename Ph3 = NoOp,
-          typename P = GemmParams>
+// CARRY (EVT_BPF, 256 x 256): bit 0, B n-half-0 fragments come in *bc (read by the previous
+// K-tile's phase 3); bit 1, phase 3 reads the next K-tile's into *bc (its region retired by a
+// phase-2 wait).
+// RT (PERS_RIA: a persistent residual GEMM whose residual is added into the accumulators by the
+// main loop instead of fetched by the epilogue; nk >= RIA_NK): K-tiles 1 .. 9 run unrolled as
+// RT = t. The odd K-tiles 1, 3, 5, 7 load the residual of one 16-column group nt = (t - 1) / 2 of
+// the wave's 128 x 64 block (8-B loads in the accumulator layout, mt 2 ph and 2 ph + 1 in phase
+// ph, right after the phase's wait, into slots mt); K-tile t + 2 adds them (mt 0-3 in phase 0,
+// 4-5 in 1, 6-7 in 2, each before that accumulator's MFMA of the K-tile) after its phase-0 wait
+// has retired the DMA issued after the last of them. Every element of column group nt thus gets
+// its residual after exactly (2 nt + 3) K-tile contributions, whatever its row: the rounding does
+// not depend on a row's position in the tile (batch-position independence). The residual's HBM
+// stream is spread over the loop instead of a 128 KB burst per tile in the epilogue. The loads
+// count in vmcnt (issue order): an odd K-tile's wait keeps its earlier phases' 2 ph loads in
+// flight besides the 8 younger DMAs, an even K-tile's the 2 (4 - ph) loads of the previous one.
+constexpr int RIA_NK = 12;
+template <int BASE, int A0, int A1, int A3>
+__device__ __forceinline__ void wait_ph(int ph) {  // (no wait in phase 2)
+  if (ph == 0) wait_vm<BASE + A0>();
+  else if (ph == 1) wait_vm<BASE + A1>();
+  else if (ph == 3) wait_vm<BASE + A3>();
+}
+struct NoRh {
+  template <typename A>
+  __device__ void add(A&, int, int) {}
+  __device__ void issue(int, int) {}
+};
+
+template <int NH>
+struct BCarry {
+  u32x4 v[NH][2];
+};
+template <int MODE, int X, int CARRY = 0, int RT = 0, bool OPEN = false, int X3 = 0,
+          typename Ph3 = NoOp, typename P = GemmParams, typename Rh = NoRh>
 __device__ __forceinline__ void big8_ktile(const P& p, char* smem,
                                            f32x4 (&acc)[GeoOf<P>::NF][GeoOf<P>::MF],
                                            int wave, int lane, int wm, int wn, int m0, int n0,
                                            int t, bool cont = false, int nm0 = 0, int nn0 = 0,
                                            Ph3 ph3 = {}, int par = 0, int npar = 0,
-                                           bool x3on = true) {
+                                           bool x3on = true, BCarry<Geo<P>::NH>* bc = nullptr,
+                                           Rh* rh = nullptr) {
   typedef Geo<P> Gm;
   constexpr int MH = Gm::MH, NH = Gm::NH;
+  constexpr bool HAS = CARRY & 1, PFN = CARRY & 2;
+  static_assert(CARRY == 0 || (Gm::BM == 256 && EVT_BPF), "carry: 256 x 256 DMA order only");
+  static_assert(!PFN || MODE < 2, "the last K-tile has no next K-tile");
+  static_assert(RT == 0 || (X3 == 0 && Gm::BM == 256 && MODE == 0 && X == 0 && RT <= 9),
+                "residual chunks: 256 x 256 steady K-tiles 1 .. 9");
+  constexpr bool RLOAD = (RT & 1) && RT <= 7, RADD = (RT & 1) && RT >= 3;
   const int frow = lane & 15, fsw = lane & 7, fg = lane >> 4;
   const EVT_LDS char* As = (const EVT_LDS char*)smem + ((t ^ par) & 1) * BIG_STAGE;
   const EVT_LDS char* Ws = As + Gm::A_TILE;
@@ -780,7 +865,8 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem,
 #pragma unroll
         for (int nt = 0; nt < NH; ++nt)
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) bf0[nt][ks] = rd(Ws, wn * Gm::WC + nt * 16 + frow, ks);
+          for (int ks = 0; ks < 2; ++ks)
+            bf0[nt][ks] = HAS ? bc->v[nt][ks] : rd(Ws, wn * Gm::WC + nt * 16 + frow, ks);
 #pragma unroll
         for (int mt = 0; mt < MH; ++mt)
 #pragma unroll
@@ -797,6 +883,13 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem,
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks)
             af[mt][ks] = rd(As, wm * Gm::WR + Gm::WR / 2 + mt * 16 + frow, ks);
+      } else if (PFN) {  // ph 3: the next K-tile's B n-half 0 (its buffer, region j = 0)
+        const EVT_LDS char* Wn =
+            (const EVT_LDS char*)smem + (((t + 1) ^ par) & 1) * BIG_STAGE + Gm::A_TILE;
+#pragma unroll
+        for (int nt = 0; nt < NH; ++nt)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) bc->v[nt][ks] = rd(Wn, wn * Gm::WC + nt * 16 + frow, ks);
       }
     };
     auto dmas = [&]() {
@@ -823,7 +916,28 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem,
     // the W n-half-1 region must have landed; its last instruction is followed by 8 younger ones
     // in the 256 x 256 order, by 7 in the paired order of the 128 x 384 geometry (big8_stage)
     constexpr int W0 = Gm::WI == 3 ? 7 : 8;
-    if (ph != 2) {
+    if (RT > 0) {  // W0 = 8 in this geometry
+      if (RLOAD) wait_ph<8, 0, 2, 6>(ph);        // this K-tile's loads of phases < ph
+      else if (RT & 1) wait_ph<8, 0, 0, 0>(ph);  // K-tile 9: none since K-tile 7
+      else wait_ph<8, 8, 6, 2>(ph);              // the previous K-tile's loads of phases >= ph
+      if (RADD) {  // column group (RT - 3) / 2, loaded two K-tiles ago
+        constexpr int NT = (RT - 3) / 2;
+        if (ph == 0) {
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) rh->add(acc[NT][mt], mt, NT);
+        } else if (ph == 1) {
+          rh->add(acc[NT][4], 4, NT);
+          rh->add(acc[NT][5], 5, NT);
+        } else if (ph == 2) {
+          rh->add(acc[NT][6], 6, NT);
+          rh->add(acc[NT][7], 7, NT);
+        }
+      }
+      if (RLOAD) {
+        rh->issue(2 * ph, (RT - 1) / 2);
+        rh->issue(2 * ph + 1, (RT - 1) / 2);
+      }
+    } else if (ph != 2) {
       if (MODE == 0) {
         if (ph == 3 && X3 > 0 && x3on) wait_vm<8 + X + X3>();
         else if (ph == 0) wait_vm<W0 + X>();
@@ -842,6 +956,11 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem,
       } else if (ph == 1) {
         wait_vm<0 + X>();
       }
+    } else if (PFN) {
+      // phase 3 reads the next K-tile's region j = 0, DMA'd 4 phases before this one: 8 younger
+      // instructions in steady state; MODE 1 issues no DMA in this phase unless cont
+      if (MODE == 0 || cont) wait_vm<8 + X>();
+      else wait_vm<6 + X>();
     }
     big8_bar();
 #if EVT_PHASE_LGKM0
@@ -875,15 +994,19 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem,
 // they are younger than every DMA that tile waits for).
 // pf: issues PFX further VMEM loads at the start of phase 3 of steady-state K-tile tpf (added to
 // that phase's wait; the following waits of the next K-tile retire one phase's DMA earlier).
+// rh (PERS_RIA, nk >= RIA_NK): the loop K-tiles carry the residual chunks (big8_ktile RT).
 template <int X, bool OPEN = false, typename Pre1 = NoOp, typename Mid = NoOp, int LX = 0,
           typename Last = NoOp, int LX3 = 0, typename Last3 = NoOp, typename P = GemmParams,
-          int PFX = 0, typename Pf = NoOp>
+          int PFX = 0, typename Pf = NoOp, typename Rh = NoRh>
 __device__ __forceinline__ void big8_loop(const P& p, char* smem,
                                           f32x4 (&acc)[GeoOf<P>::NF][GeoOf<P>::MF],
                                           int wave, int lane, int wm, int wn, int m0, int n0,
                                           int nk, bool cont = false, int nm0 = 0, int nn0 = 0,
                                           Pre1 pre1 = {}, Mid mid = {}, Last last = {},
-                                          Last3 last3 = {}, int par = 0, Pf pf = {}, int tpf = -1) {
+                                          Last3 last3 = {}, int par = 0, Pf pf = {}, int tpf = -1,
+                                          Rh* rh = nullptr) {
+  constexpr bool RIA = !std::is_same<Rh, NoRh>::value;
+  static_assert(!RIA || PFX == 0, "residual chunks and the residual L2 prefetch exclude each other");
   // K-tile t of this tile sits in buffer (t ^ par) & 1; the next tile (cont) starts at the parity
   // of stream K-tile nk
   const int npar = par ^ (nk & 1);
@@ -894,32 +1017,57 @@ __device__ __forceinline__ void big8_loop(const P& p, char* smem,
     pre1();
     big8_bar();
   }
+  // EVT_BPF carry of B n-half-0 fragments from each K-tile's phase 3 to the next one's phase 0
+  constexpr bool BPF = EVT_BPF && Geo<P>::BM == 256;
+  constexpr int CF = BPF ? 2 : 0, CM = BPF ? 3 : 0, CL = BPF ? 1 : 0;  // first / middle / last
+  BCarry<Geo<P>::NH> bc;
   if (nk >= 3) {
-    big8_ktile<0, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, false, 0, 0, {}, par);
+    big8_ktile<0, X, CF>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, false, 0, 0, {}, par, 0,
+                         true, &bc);
     mid();
     int t = 1;
+    if constexpr (RIA) {  // the launch guarantees nk >= RIA_NK: K-tiles 1 .. 9 are steady
+      auto kt = [&](auto rt) {
+        constexpr int RT = decltype(rt)::value;
+        big8_ktile<0, 0, CM, RT>(p, smem, acc, wave, lane, wm, wn, m0, n0, RT, false, 0, 0, {},
+                                 par, 0, true, &bc, rh);
+      };
+      kt(std::integral_constant<int, 1>{});
+      kt(std::integral_constant<int, 2>{});
+      kt(std::integral_constant<int, 3>{});
+      kt(std::integral_constant<int, 4>{});
+      kt(std::integral_constant<int, 5>{});
+      kt(std::integral_constant<int, 6>{});
+      kt(std::integral_constant<int, 7>{});
+      kt(std::integral_constant<int, 8>{});
+      kt(std::integral_constant<int, 9>{});
+      t = 10;
+    }
     for (; t + 2 < nk; ++t) {
       if constexpr (PFX > 0) {
         const bool on = t == tpf;  // wave-uniform
-        big8_ktile<0, 0, false, PFX>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, false, 0, 0,
-                                     [&]() { if (on) pf(); }, par, 0, on);
+        big8_ktile<0, 0, CM, 0, false, PFX>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, false, 0,
+                                         0, [&]() { if (on) pf(); }, par, 0, on, &bc);
       } else {
-        big8_ktile<0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, false, 0, 0, {}, par);
+        big8_ktile<0, 0, CM>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, false, 0, 0, {}, par, 0,
+                             true, &bc);
       }
     }
-    big8_ktile<1, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, cont, nm0, nn0, {}, par, npar);
+    big8_ktile<1, 0, CM>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, cont, nm0, nn0, {}, par,
+                         npar, true, &bc);
     last();
-    big8_ktile<2, LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1, cont, nm0, nn0,
-                                 last3, par, npar);
+    big8_ktile<2, LX, CL, 0, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1, cont, nm0,
+                                     nn0, last3, par, npar, true, &bc);
   } else if (nk == 2) {
-    big8_ktile<1, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, cont, nm0, nn0, {}, par, npar);
+    big8_ktile<1, X, CF>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, cont, nm0, nn0, {}, par,
+                         npar, true, &bc);
     last();
-    big8_ktile<2, LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, 1, cont, nm0, nn0,
-                                 last3, par, npar);
+    big8_ktile<2, LX, CL, 0, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, 1, cont, nm0, nn0,
+                                     last3, par, npar, true, &bc);
   } else {
     last();
-    big8_ktile<2, X + LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, false, 0, 0,
-                                     last3, par);
+    big8_ktile<2, X + LX, 0, 0, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, false, 0, 0,
+                                        last3, par);
   }
   if (!OPEN && wm == 0) big8_bar();
 }
@@ -1068,6 +1216,9 @@ constexpr int PERS_LDS = PERS_PART + 4096;
 constexpr int PERS_SINK = PERS_LDS + 16;        // 256 B that the residual L2 prefetch DMAs into
 constexpr int PERS_LDS_ALL = PERS_SINK + 256;
 constexpr int PERS_X = 16;                      // output stores per wave per interior tile
+// template-only flag of gemm_pers_kernel (above the EPI_ bits): residual GEMM whose residual is
+// added into the accumulators by the main loop (RiaHook), K >= 64 RIA_NK
+constexpr int PERS_RIA = 1 << 16;
 
 template <int FL>
 struct PersFlags {
@@ -1367,6 +1518,51 @@ __device__ __forceinline__ int pos_img(int m, int P) {
 }
 __device__ __forceinline__ int pos_orow(int m, int P) { return m + pos_img(m, P) + 1; }
 
+// PERS_RIA: the tile's residual, chunk (mt, nt) = rows wm 128 + mt 16 + frow, columns
+// wn 64 + nt 16 + 4 fg .. + 3 (the accumulator layout of acc[nt][mt]), 8-B buffer loads through
+// the tile's descriptor (rows past M read 0) into slot mt, added as the epilogue adds it: plain,
+// or the residual LayerNorm gamma (r resid - r mu) (beta stays in the epilogue's bias add).
+template <int FL>
+struct RiaHook {
+  __amdgpu_buffer_rsrc_t rs;
+  int vo, ldr2, rl, cl;
+  const char* smem;
+  u32x2 rv[8];
+  __device__ __forceinline__ RiaHook(const GemmParams& p, const char* sm, int wm, int wn, int lane,
+                                     int m0, int n0) : smem(sm) {
+    const int frow = lane & 15, fg = lane >> 4;
+    rl = wm * 128 + frow;
+    cl = wn * 64 + 4 * fg;
+    ldr2 = (int)p.ldr * 2;
+    rs = tile_rsrc(p.resid, p.ldr, p.M, m0, n0);
+    vo = rl * ldr2 + cl * 2;
+  }
+  __device__ __forceinline__ void issue(int mt, int nt) {
+    const int so = __builtin_amdgcn_readfirstlane(mt * 16 * ldr2 + nt * 32);
+    rv[mt] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, 0));
+  }
+  __device__ __forceinline__ void add(f32x4& a, int mt, int nt) {
+    const bf16x4 r4 = __builtin_bit_cast(bf16x4, rv[mt]);
+    if constexpr ((FL & EPI_RESLN) != 0) {
+      const f32x2 cf = ((const EVT_LDS f32x2*)(smem + PERS_COEF))[rl + mt * 16];
+      const f32x4 g = lds4((const EVT_LDS float*)(smem + PERS_COLB) + 256 + cl + 16 * nt);
+      const f32x2 rr = {cf[1], cf[1]}, nrm = {-cf[1] * cf[0], -cf[1] * cf[0]};
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const f32x2 rv2 = {(float)r4[2 * q], (float)r4[2 * q + 1]};
+        const f32x2 tt = __builtin_elementwise_fma(rr, rv2, nrm);
+        const f32x2 o = __builtin_elementwise_fma(f32x2{g[2 * q], g[2 * q + 1]}, tt,
+                                                  f32x2{a[2 * q], a[2 * q + 1]});
+        a[2 * q] = o[0];
+        a[2 * q + 1] = o[1];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] += (float)r4[j];
+    }
+  }
+};
+
 // Epilogue of one 256 x 256 tile straight from the accumulators (VALU-bound: every instruction
 // here is paid with the MFMA pipe idle, so the arithmetic is in packed form throughout):
 //   LNIN   r (acc - mu colsum) + c      2 v_pk_fma per column pair
@@ -1415,6 +1611,7 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
       ((unsigned long long*)p.pos)[((int64_t)blockIdx.x * 16 + iter) * 8 + k] = __builtin_amdgcn_s_memtime();
   };
   asm volatile("" : "+v"(lane));  // keep lane-derived addresses out of the persistent loop (VGPRs)
+  constexpr bool RIA = (FL & PERS_RIA) != 0;  // the residual is already in the accumulators
   if constexpr (DBG == 2) {  // ablation: no epilogue at all, accumulators kept live by a dead store
     float sink = 0.f;
 #pragma unroll
@@ -1505,7 +1702,7 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
     for (int k = 0; k < 4; ++k)
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) rr[k][nt] = u32x4{0u, 0u, 0u, 0u};
-  } else if constexpr ((FL & EPI_RESID) != 0) {
+  } else if constexpr ((FL & EPI_RESID) != 0 && !RIA) {
     const __amdgpu_buffer_rsrc_t rs = tile_rsrc(p.resid, p.ldr, p.M, m0, n0);
     const int vo = (rl * (int)p.ldr + cl) * 2;
 #pragma unroll
@@ -1562,7 +1759,7 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       f32x4 v[2] = {acc[nt][2 * k], acc[nt][2 * k + 1]};
-      if constexpr ((FL & (EPI_RESID | EPI_POS)) != 0) {
+      if constexpr (((FL & EPI_RESID) != 0 && !RIA) || (FL & EPI_POS) != 0) {
         const bf16x8 r8 = __builtin_bit_cast(bf16x8, rr[k][nt]);
         const f32x2 rrow = {rc[k][1], rc[k][1]}, nrm = {-rc[k][1] * rc[k][0], -rc[k][1] * rc[k][0]};
 #pragma unroll
@@ -1791,7 +1988,11 @@ template <int FL, int DBG, bool PADN, int ROLE, typename P = GemmParams>
 __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* smem,
                                          ChainCtx& cx) {
   // a quarter of the residual before the last K-tile (out-proj 160 -> 153 us); DBG 20: A/B without
-  constexpr int ER = ((FL & EPI_RESID) != 0 && DBG != 7 && DBG != 20 && DBG != 18)
+  // (PERS_RIA: none, the main loop adds the residual)
+  constexpr bool RIA = (FL & PERS_RIA) != 0;
+  static_assert(!RIA || ((FL & EPI_RESID) != 0 && (FL & EPI_POS) == 0 && ROLE == 0 && DBG == 0),
+                "residual chunks: standalone persistent residual GEMMs (gemm_chain_launch)");
+  constexpr int ER = ((FL & EPI_RESID) != 0 && !RIA && DBG != 7 && DBG != 20 && DBG != 18)
                          ? (DBG == 21 ? 1 : 2) : 0;  // DBG 21: A/B with one quarter
   constexpr bool SC1 = (ROLE & 1) != 0;
   constexpr bool WAITS = (ROLE & 2) != 0;
@@ -1864,7 +2065,12 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
       __builtin_amdgcn_global_load_lds((const bf16*)p.resid + (int64_t)gm * p.ldr + gn,
                                        (EVT_LDS char*)smem + PERS_SINK, 4, 0, 0);
     };
-    constexpr int PFX = ((FL & EPI_RESID) != 0 && EVT_RES_PF > 0) ? 1 : 0;
+    constexpr int PFX = ((FL & EPI_RESID) != 0 && !RIA && EVT_RES_PF > 0) ? 1 : 0;
+    auto make_rh = [&]() {
+      if constexpr (RIA) return RiaHook<FL>(p, smem, wm, wn, ln, m0, n0);
+      else return NoRh{};
+    };
+    auto rh = make_rh();
     const int tpf = PFX ? nk - 1 - EVT_RES_PF : -1;
     if (early) {
       // this tile's LayerNorm coefficients by wave group 1 while it waits for group 0's first
@@ -1881,7 +2087,7 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
         big8_loop<PERS_X, true, decltype(pre1), decltype(mid), (ER > 0 ? 4 : 0), decltype(last),
                   (ER > 1 ? 4 : 0), decltype(last3), P, PFX, decltype(pf)>(
             p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM, ntn * BIG_BN, pre1, mid,
-            last, last3, par, pf, tpf);
+            last, last3, par, pf, tpf, &rh);
       stamp(1);
       if (has_next && !cont) {
         if constexpr (WAITS) {
@@ -2595,7 +2801,8 @@ bool gemm_lab_pers_variant(int v) {
 
 bool use_pers(const GemmParams& p, int flags) {
   const int v = g_gemm_variant;
-  if (v != 0 && v != 9 && v != 16 && v != 31 && v != 32 && !gemm_lab_pers_variant(v)) return false;
+  if (v != 0 && v != 9 && v != 16 && v != 31 && v != 32 && v != 33 && !gemm_lab_pers_variant(v))
+    return false;
   // timeline variants stamp s_memtime through p.pos: never on the patch GEMM (p.pos = the table)
   if ((v == 13 || v == 15) && (flags & EPI_POS)) return false;
   if (p.N % 8 || p.vec_ok < 2) return false;
@@ -2604,6 +2811,24 @@ bool use_pers(const GemmParams& p, int flags) {
   // POS: the bf16 copy of the position table rides in resid / ldr (else the staged-epilogue kernel)
   if ((flags & EPI_POS) && (!p.resid || p.ldr % 8 || p.P <= 0 || p.M >= (1 << 22))) return false;
   return true;
+}
+
+// residual GEMMs with K >= 64 RIA_NK: the residual added by the main loop (PERS_RIA);
+// variant 33 keeps the epilogue residual (A/B in one process)
+template <int FL>
+bool launch_pers_ria(const GemmParams& q, int G, int total, hipStream_t s) {
+  if constexpr ((FL & EPI_RESID) != 0 && (FL & (EPI_POS | EPI_GATHER | EPI_SPLIT)) == 0) {
+    if (g_gemm_variant == 33 || q.K % 64 || q.K / 64 < RIA_NK) return false;
+    if (q.N % BIG_BN == 0)
+      hipLaunchKernelGGL((gemm_pers_kernel<FL | PERS_RIA, 0, false>), dim3(G), dim3(512), 0, s, q,
+                         total);
+    else
+      hipLaunchKernelGGL((gemm_pers_kernel<FL | PERS_RIA>), dim3(G), dim3(512), 0, s, q, total);
+    return true;
+  } else {
+    (void)q, (void)G, (void)total, (void)s;
+    return false;
+  }
 }
 
 template <int FL>
@@ -2643,6 +2868,8 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_pers_kernel<(FL & ~(EPI_GELU | EPI_GELU_ERF)), 0, false>), dim3(G),
                        dim3(512), 0, s, q, total);
 #endif
+  else if (launch_pers_ria<FL>(q, G, total, s))
+    ;
   else if (p.N % BIG_BN == 0)
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 0, false>), dim3(G), dim3(512), 0, s, q, total);
   else
@@ -2884,7 +3111,7 @@ int device_cus() { return num_cus(); }
 void gemm_set_variant(int v) { g_gemm_variant = v; }
 bool gemm_variant_supported(int v) {
   return v == 0 || v == 1 || v == 2 || v == 6 || v == 8 || v == 9 || v == 16 || v == 30 || v == 31 ||
-         v == 32 ||
+         v == 32 || v == 33 ||
          gemm_lab_pers_variant(v)
 #ifdef EVT_GEMM_LAB
          || v == 106 || v == 108
@@ -2903,7 +3130,13 @@ void gemm_sk_bind(void* ws, GemmParams& p) {
 hipError_t gemm_chain_launch(int dtype, int fa, const GemmParams& pa, int fb, const GemmParams& pb,
                              const ChainWords& cw, hipStream_t s) {
   constexpr int RES = EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS;
-  if (dtype != DT_BF16 || g_gemm_variant != 0 || fa != RES || !cw.sync) return hipErrorNotSupported;
+  if (dtype != DT_BF16 || (g_gemm_variant != 0 && g_gemm_variant != 33) || fa != RES || !cw.sync)
+    return hipErrorNotSupported;
+  // where the standalone out-proj adds its residual in the main loop (PERS_RIA) the pair runs
+  // separately: the producer's extra registers make hipcc spill the ticket atomic's destination
+  // VGPR before the atomic returns (an asm output; measured round 4: a broken tile walk), and a
+  // producer without PERS_RIA would not be bitwise the separate launches
+  if (g_gemm_variant == 0 && pa.K % 64 == 0 && pa.K / 64 >= RIA_NK) return hipErrorNotSupported;
   // only where both GEMMs would take the 256 x 256 persistent kernel on their own (bitwise the
   // separate launches)
   if (pa.M != pb.M || pa.N % BIG_BN || pb.N % BIG_BN || pa.K / 64 < 3 || pb.K / 64 < 3 ||
