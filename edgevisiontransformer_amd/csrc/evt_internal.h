@@ -263,7 +263,7 @@ int gemm_variant();  // the calling thread's evt_set_gemm_variant value (0 = aut
 // automatic kernel selection (0; 30 / 31 only steer the 128 x 384 tiles): fused kernels allowed
 inline bool gemm_auto() {
   const int v = gemm_variant();
-  return v == 0 || v == 30 || v == 31 || v == 32 || v == 33;
+  return v == 0 || v == 30 || v == 31 || v == 32 || v == 33;  // (33: EVT_RIA lab builds)
 }
 bool gemm_variant_supported(int v);  // compiled into this build (lab variants: EVT_GEMM_LAB)
 

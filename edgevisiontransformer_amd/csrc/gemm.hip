@@ -510,7 +510,7 @@ bool use_big(const GemmParams& p, int flags) {
   if (!(flags & EPI_OUT_F32) && p.vec_ok < 2) return false;  // big epilogue: 16-B bf16 stores only
   // 31: automatic without 128 x 384; 32: automatic with the round-3 rule (>= 256 big tiles)
   const int v = (g_gemm_variant == 31 || g_gemm_variant == 32 || g_gemm_variant == 33)
-                    ? 0 : g_gemm_variant;
+                    ? 0 : g_gemm_variant;  // (33: EVT_RIA lab builds)
   if (v == 1) return false;
   if (v >= 2) return true;
   // 256x256 tiles unless their rounds cost more: time in 256-tile units, the 128x128 kernel at a
@@ -688,13 +688,14 @@ __device__ __forceinline__ const char* gather_addr(const GemmParams& p, int gm, 
   return (const char*)p.A + (src * p.lda + c) * 2;
 }
 
-// 256 x 256 plain loaders: the DMA pieces are buffer_load ... lds through a per-tile descriptor
-// (SGPR base at the panel's first row, rows past M read zeros) with a tile-invariant 32-bit lane
-// offset and the K-tile offset in soffset (1), instead of global_load_lds on a 64-bit address
-// formed per piece (0: ~8 VALU per piece, 64 per K-tile per wave, in the issue slots beside the
-// partner wave's MFMAs)
+// 256 x 256 plain loaders (lab A/B): the DMA pieces as buffer_load ... lds through a per-tile
+// descriptor (SGPR base at the panel's first row, rows past M read zeros) with one tile-invariant
+// 32-bit lane offset per operand and the K-tile / row-group offset in soffset (1), instead of
+// global_load_lds on a 64-bit address formed per piece (0, the product: ~8 VALU per piece).
+// Measured round 4: 16-24 fewer VGPRs in every persistent kernel and no spills, yet DeiT-base
+// 27.7k vs 28.9k img/s in 3 of 3 alternating same-box runs (scripts/gpu_r4_ria.sh): not kept
 #ifndef EVT_BDMA
-#define EVT_BDMA 1
+#define EVT_BDMA 0
 #endif
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t dma_rsrc(const void* mat, int64_t ld, int rows,
                                                           int r0) {
@@ -818,6 +819,13 @@ __device__ __forceinline__ void big8_prologue(const P& p, char* smem, int wave, 
 // count in vmcnt (issue order): an odd K-tile's wait keeps its earlier phases' 2 ph loads in
 // flight besides the 8 younger DMAs, an even K-tile's the 2 (4 - ph) loads of the previous one.
 constexpr int RIA_NK = 12;
+// (lab A/B, EVT_LAB_DEFS=-DEVT_RIA=1: measured round 4 with the buffer-descriptor loader, where
+// it fits in registers: DeiT-base 26.5k vs 27.7k img/s without it in 3 of 3 alternating runs; with
+// the global_load_lds loader it spills in the loop. Not kept: the product fetches the residual in
+// the epilogue)
+#ifndef EVT_RIA
+#define EVT_RIA 0
+#endif
 template <int BASE, int A0, int A1, int A3>
 __device__ __forceinline__ void wait_ph(int ph) {  // (no wait in phase 2)
   if (ph == 0) wait_vm<BASE + A0>();
@@ -2813,11 +2821,11 @@ bool use_pers(const GemmParams& p, int flags) {
   return true;
 }
 
-// residual GEMMs with K >= 64 RIA_NK: the residual added by the main loop (PERS_RIA);
-// variant 33 keeps the epilogue residual (A/B in one process)
+// (EVT_RIA lab builds) residual GEMMs with K >= 64 RIA_NK: the residual added by the main loop
+// (PERS_RIA); variant 33 keeps the epilogue residual (A/B in one process)
 template <int FL>
 bool launch_pers_ria(const GemmParams& q, int G, int total, hipStream_t s) {
-  if constexpr ((FL & EPI_RESID) != 0 && (FL & (EPI_POS | EPI_GATHER | EPI_SPLIT)) == 0) {
+  if constexpr (EVT_RIA && (FL & EPI_RESID) != 0 && (FL & (EPI_POS | EPI_GATHER | EPI_SPLIT)) == 0) {
     if (g_gemm_variant == 33 || q.K % 64 || q.K / 64 < RIA_NK) return false;
     if (q.N % BIG_BN == 0)
       hipLaunchKernelGGL((gemm_pers_kernel<FL | PERS_RIA, 0, false>), dim3(G), dim3(512), 0, s, q,
@@ -3111,7 +3119,7 @@ int device_cus() { return num_cus(); }
 void gemm_set_variant(int v) { g_gemm_variant = v; }
 bool gemm_variant_supported(int v) {
   return v == 0 || v == 1 || v == 2 || v == 6 || v == 8 || v == 9 || v == 16 || v == 30 || v == 31 ||
-         v == 32 || v == 33 ||
+         v == 32 || (EVT_RIA && v == 33) ||
          gemm_lab_pers_variant(v)
 #ifdef EVT_GEMM_LAB
          || v == 106 || v == 108
@@ -3130,13 +3138,15 @@ void gemm_sk_bind(void* ws, GemmParams& p) {
 hipError_t gemm_chain_launch(int dtype, int fa, const GemmParams& pa, int fb, const GemmParams& pb,
                              const ChainWords& cw, hipStream_t s) {
   constexpr int RES = EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS;
-  if (dtype != DT_BF16 || (g_gemm_variant != 0 && g_gemm_variant != 33) || fa != RES || !cw.sync)
+  if (dtype != DT_BF16 || (g_gemm_variant != 0 && !(EVT_RIA && g_gemm_variant == 33)) || fa != RES ||
+      !cw.sync)
     return hipErrorNotSupported;
   // where the standalone out-proj adds its residual in the main loop (PERS_RIA) the pair runs
   // separately: the producer's extra registers make hipcc spill the ticket atomic's destination
   // VGPR before the atomic returns (an asm output; measured round 4: a broken tile walk), and a
   // producer without PERS_RIA would not be bitwise the separate launches
-  if (g_gemm_variant == 0 && pa.K % 64 == 0 && pa.K / 64 >= RIA_NK) return hipErrorNotSupported;
+  if (EVT_RIA && g_gemm_variant == 0 && pa.K % 64 == 0 && pa.K / 64 >= RIA_NK)
+    return hipErrorNotSupported;
   // only where both GEMMs would take the 256 x 256 persistent kernel on their own (bitwise the
   // separate launches)
   if (pa.M != pb.M || pa.N % BIG_BN || pb.N % BIG_BN || pa.K / 64 < 3 || pb.K / 64 < 3 ||

@@ -465,9 +465,7 @@ int evt_attention_mx8(const void* qkv, int64_t ldq, void* q8, int64_t ldq8, uint
  * tiles with the plain / interleaved / 8-phase ping-pong main loop whenever the packed width
  * allows, 9 = tile-persistent, 16 = stream-K persistent where it applies, 30 = the 128 x 384
  * persistent tiles wherever the width allows (multiple of 384), 31 = automatic without them, 32 =
- * automatic with the round-3 tile rule (256 x 256 tiles only from 256 of them up), 33 =
- * automatic with the residual of out-proj / FC2 fetched by the epilogue (K >= 768 otherwise adds
- * it in the main loop). Builds with
+ * automatic with the round-3 tile rule (256 x 256 tiles only from 256 of them up). Builds with
  * EVT_LAB=1 (-DEVT_GEMM_LAB) also accept the ablation / timeline variants 10, 11, 13, 15, 17-25,
  * 106, 108; other values return EVT_EINVAL. */
 int evt_set_gemm_variant(int variant);

@@ -17,16 +17,6 @@ from edgevisiontransformer_amd import _lib
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True)
-def _epilogue_residual_variant():
-    """The chain runs where the separate out-proj fetches its residual in the epilogue (gemm
-    variant 33 at K = 768; gemm.hip gemm_chain_launch): set for this thread, restored after."""
-    lib = _lib.load_library()
-    lib.evt_set_gemm_variant(33)
-    yield
-    lib.evt_set_gemm_variant(0)
-
-
 def _model_and_ref(gpu, batch):
     from edgevisiontransformer_amd.modeling.models.vit import build_named
     m = build_named("deit_base", dtype="bf16", seed=3, max_batch=batch)
@@ -108,18 +98,3 @@ def test_chain_wait_timeout_is_reported(gpu):
         m(img)
     m.set_chain_spin(-1)
     assert torch.equal(m(img), ref)
-
-
-def test_chain_declines_where_the_residual_is_added_in_the_main_loop(gpu):
-    """Automatic selection (variant 0): DeiT-base's out-proj (K = 768) adds its residual in the
-    main loop, so the chained launch is declined and the fused forward is the separate launches'
-    forward, bitwise."""
-    lib = _lib.load_library()
-    lib.evt_set_gemm_variant(0)
-    m, img, ref = _model_and_ref(gpu, 256)
-    out = torch.empty_like(ref)
-    m.set_chain_spin(0)  # a chained launch would report its (forced) hand-off timeout
-    m.forward_into(img, out)
-    torch.cuda.synchronize()
-    m.check_status()
-    assert torch.equal(out, ref)
