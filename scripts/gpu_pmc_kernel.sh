@@ -22,6 +22,21 @@ GRBM_GUI_ACTIVE GRBM_COUNT TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD
 FETCH_SIZE
 WRITE_SIZE
 G
+timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $O/kt -o run \
+  -- python3 $R/bench.py $ARGS --cpu-seconds 0 --no-probe --steps 2 --warmup 1 > $O/kt.log 2>&1 || exit 1
+python3 - "$O" "$KNAME" <<'PY'
+import csv, glob, collections, sys
+O, kname = sys.argv[1], sys.argv[2]
+by = collections.defaultdict(list)  # per-dispatch durations by grid size (one group per stage)
+for f in glob.glob(f"{O}/kt/**/*kernel_trace.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if kname in r["Kernel_Name"]:
+            by[r.get("Grid_Size_X", r.get("Grid_Size", "?"))].append(
+                (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+for g, v in sorted(by.items(), key=lambda kv: -len(kv[1])):
+    v.sort()
+    print(f"grid {g}: {len(v)} launches, median {v[len(v)//2]:.1f} us, min {v[0]:.1f}")
+PY
 python3 - "$O" "$KNAME" <<'PY'
 import csv, glob, collections, json, sys
 O, kname = sys.argv[1], sys.argv[2]
