@@ -40,6 +40,9 @@ PER_FILE_FLAGS["attention.hip"] = PER_FILE_FLAGS["attention.hip"] + ["-fno-honor
 # qkv_attn.hip: no NaN operands on the path, so fmaxf on raw MFMA results needs no canonicalising
 # v_max per element before the softmax max tree (-inf masking is unaffected)
 PER_FILE_FLAGS["qkv_attn.hip"] = ["-fno-honor-nans"]
+# swin.hip: the same for the window-attention softmax (finite scores, -inf masks; 32 canonicalising
+# v_max per wave before, round-4 counters)
+PER_FILE_FLAGS["swin.hip"] = PER_FILE_FLAGS["swin.hip"] + ["-fno-honor-nans"]
 
 
 def _hipcc() -> str:

@@ -1382,8 +1382,7 @@ int evt_swin_create(const evt_swin_desc* desc, const float* const* w, int n_weig
         bl.shift = (j % 2 == 1 && st.R > 7) ? 3 : 0;  // SW-MSA on odd blocks; none at R == window
         const int C = st.C;
         EVT_RC(make_dense(m, &bl.qkv, w[k + 2], w[k + 3], C, 3 * C, s, w[k + 0], w[k + 1]));
-        EVT_RC(dev_alloc(m, (void**)&bl.bias,
-                         (size_t)(bl.shift ? 4 : 1) * st.H * 49 * 64 * sizeof(float)));
+        EVT_RC(dev_alloc(m, (void**)&bl.bias, rpb_table_floats(st.H, 7, bl.shift) * sizeof(float)));
         EVT_HIP(rpb_dense_launch(w[k + 4], st.H, 7, bl.shift, bl.bias, s), "relative position bias");
         EVT_RC(make_dense(m, &bl.proj, w[k + 5], w[k + 6], C, C, s));
         EVT_RC(make_dense(m, &bl.fc1, w[k + 9], w[k + 10], C, st.mlp, s, w[k + 7], w[k + 8]));
@@ -1601,7 +1600,7 @@ int evt_window_attention(int dtype, const void* qkv, int64_t ldq, void* out, int
     return fail(EVT_EINVAL, "bad window-attention shape (R % 7 == 0, head size 32, 0 <= shift < 7)");
   hipStream_t s = (hipStream_t)stream;
   float* dense_bias = nullptr;
-  EVT_HIP(hipMallocAsync((void**)&dense_bias, (size_t)(shift ? 4 : 1) * H * 49 * 64 * sizeof(float), s),
+  EVT_HIP(hipMallocAsync((void**)&dense_bias, rpb_table_floats(H, 7, shift) * sizeof(float), s),
           "malloc bias");
   EVT_HIP(rpb_dense_launch(rpb, H, 7, shift, dense_bias, s), "relative position bias");
   SwinAttnParams ap{qkv, ldq, out, ldo, dense_bias, B, R, R / 7, C, H, shift,

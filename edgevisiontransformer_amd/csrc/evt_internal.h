@@ -201,6 +201,8 @@ hipError_t ln_rows_launch(int dtype, const void* x, int64_t ld, void* y, const f
 hipError_t merge_launch(int dtype, const void* x, int64_t ldx, int B, int R, int C, void* out,
                         float* stats, int nslots, hipStream_t s);
 // dense bias+mask tables [types][H][49][64] (types = 4 when shift > 0, else 1)
+// floats of the tables rpb_dense_launch writes (dense [types][H][49][64] + compact [H][192])
+size_t rpb_table_floats(int H, int w, int shift);
 hipError_t rpb_dense_launch(const float* table, int H, int w, int shift, float* dense,
                             hipStream_t s);
 hipError_t window_attn_launch(int dtype, const SwinAttnParams& p, hipStream_t s);

@@ -242,6 +242,19 @@ __global__ void rpb_dense_kernel(const float* __restrict__ table, int H, int w, 
   dense[e] = v;
 }
 
+// Compact relative-position table per head (the bf16 window kernel's bias source): RPB_CROW
+// floats per head, entries 0 .. 168 = table[r][h] * log2(e), stored after the dense tables.
+constexpr int RPB_CROW = 192;
+__host__ __device__ __forceinline__ const float* rpb_compact(const float* dense, int H, int shift) {
+  return dense + (size_t)(shift ? 4 : 1) * H * 49 * 64;
+}
+__global__ void rpb_compact_kernel(const float* __restrict__ table, int H, float* __restrict__ out) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= H * RPB_CROW) return;
+  const int h = e / RPB_CROW, r = e - h * RPB_CROW;
+  out[e] = r < 169 ? table[r * H + h] * kLog2e : 0.f;
+}
+
 // Row of window-local token t (t < 49) of window `win` of image b, with the cyclic shift; and
 // the bias / mask table type of the window.
 struct WinGeom {
@@ -266,56 +279,124 @@ struct WinGeom {
   __device__ __forceinline__ int type() const { return wtype; }
 };
 
+// Butterfly max / sum over lanes l ^ 16 and l ^ 32 on the VALU: v_permlane16_swap / 32_swap of a
+// value with itself leave the two halves of each row pair (of the wave) in the two results, so one
+// max / add gives every lane the reduction (no LDS round trip as with ds_bpermute).
+__device__ __forceinline__ float bfly_max_16_32(float x) {
+  unsigned u = __builtin_bit_cast(unsigned, x);
+  const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  x = fmaxf(__builtin_bit_cast(float, (unsigned)a[0]), __builtin_bit_cast(float, (unsigned)a[1]));
+  u = __builtin_bit_cast(unsigned, x);
+  const auto c = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)c[0]), __builtin_bit_cast(float, (unsigned)c[1]));
+}
+__device__ __forceinline__ float bfly_sum_16_32(float x) {
+  unsigned u = __builtin_bit_cast(unsigned, x);
+  const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  x = __builtin_bit_cast(float, (unsigned)a[0]) + __builtin_bit_cast(float, (unsigned)a[1]);
+  u = __builtin_bit_cast(unsigned, x);
+  const auto c = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (unsigned)c[0]) + __builtin_bit_cast(float, (unsigned)c[1]);
+}
+
 // bf16 window attention. 4 waves per block, wave = one (image, window, head); head size 32,
 // window 7x7 = 49 tokens padded to 64 (4 tiles of 16). Q / K fragments are 16-B loads straight
-// from the QKV rows; V goes to the wave's 4 KiB of LDS (glds, chunk swizzle (row >> 2) & 3) for
-// the transposed ds_read_b64_tr_b16 reads of the V^T operand.
+// from the QKV rows; V goes to the wave's 4 KiB of LDS (LDS-DMA, chunk swizzle (row >> 2) & 3) for
+// the transposed ds_read_b64_tr_b16 reads of the V^T operand. Every global access goes through a
+// buffer descriptor of the image (SGPR base) with a 32-bit row offset per lane and the q / k / v
+// column block in soffset.
+// The relative position bias comes from the head's compact table (169 entries x log2 e, 768 B,
+// LDS-DMA'd per wave): bias(q, k) = T[(qi - ki + 6) 13 + (qj - kj + 6)] = T[a(q) - b(k)] with
+// a(q) = 6 qi + q + 84, b(k) = 6 ki + k, one ds_read_b32 per score; the SW-MSA region mask (and the
+// keys past 49) set the score to -inf (the reference's -100 leaves e^-100 relative weights, below
+// fp32 resolution against the row maximum's 1). Round-4 counters (profiles/r04_pmc_swin_*): the
+// texture-address unit was busy 75 % of the kernel, half of that stalled on the L1, and the
+// kernel without its dense-table bias reads (16 x 16 B per lane per wave, L2 hits) ran 25 %
+// faster: those reads are gone; the VALU butterflies and v_rcp_f32 cut its VALU count by 29 %.
 __global__ __launch_bounds__(256) void window_attn_bf16_kernel(SwinAttnParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * 64 * 64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t pair = (int64_t)blockIdx.x * 4 + wave;
+  __shared__ __attribute__((aligned(16))) char smem[4 * 64 * 64 + 4 * 768];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: scalar index math
+  const int pair = blockIdx.x * 4 + wave;  // (B * windows * H < 2^31: checked at launch)
   const int nw = p.nwx * p.nwx;
-  if (pair >= (int64_t)p.B * nw * p.H) return;
-  const int h = (int)(pair % p.H);
-  const int64_t bw = pair / p.H;
-  const int win = (int)(bw % nw), b = (int)(bw / nw);
-  const WinGeom G(p.R, p.nwx, p.shift, b, win);
-  const bf16* qkv = (const bf16*)p.qkv;
+  if (pair >= p.B * nw * p.H) return;
+  const int h = pair % p.H;
+  const int bw = pair / p.H;
+  const int win = bw % nw, b = bw / nw;
+  const int R = p.R, s0 = p.shift;
+  const int wy = win / p.nwx, wx = win - wy * p.nwx;
+  const int y0 = wy * 7 + s0, x0 = wx * 7 + s0;
+  const int wtype = s0 ? (wy == p.nwx - 1 ? 2 : 0) + (wx == p.nwx - 1 ? 1 : 0) : 0;
+  // image-local raster row of window token t (with the cyclic shift)
+  auto lrow = [&](int t) {
+    const int i = (t * 37) >> 8, j = t - 7 * i;  // t / 7 for t < 64
+    int y = y0 + i, x = x0 + j;
+    if (y >= R) y -= R;
+    if (x >= R) x -= R;
+    return y * R + x;
+  };
+  const int ldq2 = (int)p.ldq * 2, ldo2 = (int)p.ldo * 2;
+  const int64_t img0 = (int64_t)b * R * R;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (char*)const_cast<void*>(p.qkv) + img0 * ldq2, 0, R * R * ldq2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+      (char*)p.out + img0 * ldo2, 0, R * R * ldo2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(rpb_compact(p.bias, p.H, s0)) + h * RPB_CROW, 0, RPB_CROW * 4, 0x00020000);
   const int g = lane >> 4, c16 = lane & 15;
   EVT_LDS char* Vs = (EVT_LDS char*)smem + wave * 4096;
+  EVT_LDS char* Ts = (EVT_LDS char*)smem + 4 * 4096 + wave * 768;
+  const int C2 = p.C * 2;
 
+  // the head's compact bias table -> LDS (3 x 64 lanes x 4 B)
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, Ts + i * 256, 4, lane * 4, i * 256, 0, 0);
   // V rows (keys) -> LDS: instruction i covers rows 16 i + (lane >> 2), 16-B chunk lane & 3
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = 16 * i + (lane >> 2), ch = (lane & 3) ^ ((r >> 2) & 3);
-    const int64_t gr = G.row(min(r, 48));
-    glds16(qkv + gr * p.ldq + 2 * p.C + h * 32 + ch * 8, Vs + i * 1024);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, Vs + i * 1024, 16,
+                                             lrow(min(r, 48)) * ldq2 + (h * 32 + ch * 8) * 2,
+                                             2 * C2, 0, 0);
   }
   // Q and K fragments: tile i, lane (token 16 i + c16, d 8 g .. 8 g + 7)
   u32x4 qf[4], kf[4];
-  int64_t qrow[4];
+  int qoff[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int t = min(16 * i + c16, 48);
-    qrow[i] = G.row(t);
-    const bf16* rp = qkv + qrow[i] * p.ldq + h * 32 + 8 * g;
-    qf[i] = *(const u32x4*)rp;
-    kf[i] = *(const u32x4*)(rp + p.C);
+    const int lr = lrow(t);
+    qoff[i] = lr * ldo2 + (h * 32 + 4 * g) * 2;  // query token t's output row, this lane's columns
+    const int vo = lr * ldq2 + (h * 32 + 8 * g) * 2;
+    qf[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, 0));
+    kf[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, C2, 0));
   }
-  // bias + mask rows of all four query tiles, in flight with the Q / K / V loads
-  const float* bias_h = p.bias + ((int64_t)G.type() * p.H + h) * 49 * 64;
-  f32x4 bvs[4][4];
+  // per-lane table offsets b(k) of its 16 keys k = 16 kt + 4 g + j (keys past 48 read key 48's:
+  // masked below) and, for SW-MSA windows, their region codes (bit 0: lower part of the last
+  // window row, bit 1: right part of the last window column), one byte per j
+  int kofs[4][4];
+  unsigned kc[4] = {0u, 0u, 0u, 0u};
+  const int cut = 7 - s0;
+  const bool lr_ = wtype & 2, lc_ = wtype & 1;
 #pragma unroll
-  for (int qt = 0; qt < 4; ++qt)
+  for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-      bvs[qt][kt] = *(const f32x4*)(bias_h + (int64_t)min(16 * qt + c16, 48) * 64 + 4 * g + 16 * kt);
+    for (int j = 0; j < 4; ++j) {
+      const int k = min(16 * kt + 4 * g + j, 48), ki = (k * 37) >> 8, kj = k - 7 * ki;
+      kofs[kt][j] = (6 * ki + k) * 4;
+      kc[kt] |= (unsigned)((lr_ && ki >= cut ? 1 : 0) | (lc_ && kj >= cut ? 2 : 0)) << (8 * j);
+    }
   wait_vmcnt0();
 
   const int tq = (lane >> 2) & 3, tp = lane & 3;
+  const float NEG = -INFINITY;
 #pragma unroll
   for (int qt = 0; qt < 4; ++qt) {
     const int q = 16 * qt + c16;
+    const int qq = min(q, 48), qi = (qq * 37) >> 8, qj = qq - 7 * qi;
+    const EVT_LDS char* Tq = Ts + (6 * qi + qq + 84) * 4;
+    const unsigned cq = ((lr_ && qi >= cut ? 1u : 0u) | (lc_ && qj >= cut ? 2u : 0u)) * 0x01010101u;
     f32x4 s[4];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
@@ -324,33 +405,39 @@ __global__ __launch_bounds__(256) void window_attn_bf16_kernel(SwinAttnParams p)
                                                       __builtin_bit_cast(bf16x8, qf[qt]), acc, 0,
                                                       0, 0);
     }
-    // s[kt][j] = S^T[key 16 kt + 4 g + j][query q]: scores in the log2 domain + bias (incl. the
-    // shift mask and -inf past key 49) on packed pairs; max over canonical (computed) values
+    // s[kt][j] = S^T[key 16 kt + 4 g + j][query q]: scores in the log2 domain + bias on packed
+    // pairs, then the masks
     const f32x2 sc2 = {p.scale_log2, p.scale_log2};
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
-      const f32x4 bv = bvs[qt][kt];
+      f32x4 bv;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bv[j] = *(const EVT_LDS float*)(Tq - kofs[kt][j]);
       const f32x2 lo = f32x2{s[kt][0], s[kt][1]} * sc2 + f32x2{bv[0], bv[1]};
       const f32x2 hi = f32x2{s[kt][2], s[kt][3]} * sc2 + f32x2{bv[2], bv[3]};
       s[kt] = f32x4{lo[0], lo[1], hi[0], hi[1]};
-    }
-    float mx = -INFINITY;
+      if (wtype) {  // SW-MSA window on the last row / column: keys of another region
+        const unsigned x = kc[kt] ^ cq;
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-      mx = fmaxf(fmaxf(mx, fmaxf(s[kt][0], s[kt][1])), fmaxf(s[kt][2], s[kt][3]));
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    float sum = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float e = __builtin_amdgcn_exp2f(s[kt][j] - mx);
-        s[kt][j] = e;
-        sum += e;
+        for (int j = 0; j < 4; ++j)
+          if ((x >> (8 * j)) & 3u) s[kt][j] = NEG;
       }
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)  // keys 49 .. 63 (the padding of tile 3: all but key 48)
+      if (4 * g + j > 0) s[3][j] = NEG;
+    float m4[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) m4[kt] = fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3]));
+    const float mx = bfly_max_16_32(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3])));
+    float p4[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s[kt][j] = __builtin_amdgcn_exp2f(s[kt][j] - mx);
+      p4[kt] = (s[kt][0] + s[kt][1]) + (s[kt][2] + s[kt][3]);
+    }
+    const float sum = bfly_sum_16_32((p4[0] + p4[1]) + (p4[2] + p4[3]));
 
     f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -377,12 +464,16 @@ __global__ __launch_bounds__(256) void window_attn_bf16_kernel(SwinAttnParams p)
     }
     // o[dt][j] = O^T[d = 16 dt + 4 g + j][query q]
     if (q < 49) {
-      const float inv = 1.0f / sum;
-      bf16* op = (bf16*)p.out + qrow[qt] * p.ldo;
+      const float inv = __builtin_amdgcn_rcpf(sum);
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) store4(op + h * 32 + 16 * dt + 4 * g, o[dt] * inv);
+      for (int dt = 0; dt < 2; ++dt) {
+        const f32x4 v = o[dt] * inv;
+        const bf16x4 ob = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, ob), ro, qoff[qt], 32 * dt, 0);
+      }
       if (h == 0)  // pad columns [C, ldo) of the attention output (the proj GEMM's K padding)
-        for (int c = p.C + 4 * g; c < p.ldo; c += 16) store4(op + c, f32x4{0.f, 0.f, 0.f, 0.f});
+        for (int c = p.C + 4 * g; c < p.ldo; c += 16)
+          __builtin_amdgcn_raw_buffer_store_b64(u32x2{0u, 0u}, ro, qoff[qt] + (c - 4 * g) * 2, 0, 0);
     }
   }
 }
@@ -1121,7 +1212,14 @@ hipError_t rpb_dense_launch(const float* table, int H, int w, int shift, float* 
   const int n = (shift ? 4 : 1) * H * w * w * 64;
   hipLaunchKernelGGL(rpb_dense_kernel, dim3((n + 255) / 256), dim3(256), 0, s, table, H, w, shift,
                      dense);
+  if (w == 7)  // + the compact per-head tables of the bf16 window kernel
+    hipLaunchKernelGGL(rpb_compact_kernel, dim3((H * RPB_CROW + 255) / 256), dim3(256), 0, s, table,
+                       H, const_cast<float*>(rpb_compact(dense, H, shift)));
   return hipGetLastError();
+}
+
+size_t rpb_table_floats(int H, int w, int shift) {
+  return (size_t)(shift ? 4 : 1) * H * w * w * 64 + (size_t)H * RPB_CROW;
 }
 
 hipError_t window_attn_launch(int dtype, const SwinAttnParams& p, hipStream_t s) {
@@ -1131,6 +1229,10 @@ hipError_t window_attn_launch(int dtype, const SwinAttnParams& p, hipStream_t s)
     return hipErrorInvalidValue;
   const int64_t pairs = (int64_t)p.B * p.nwx * p.nwx * p.H;
   const dim3 grid((unsigned)((pairs + 3) / 4));
+  // bf16 kernel: 32-bit (image, window, head) index and per-image 32-bit buffer offsets
+  if (dtype == DT_BF16 && (pairs + 4 >= (int64_t)1 << 31 ||
+                           (int64_t)p.R * p.R * std::max(p.ldq, p.ldo) * 2 >= (int64_t)1 << 31))
+    return hipErrorInvalidValue;
   if (dtype == DT_BF16)
     hipLaunchKernelGGL(window_attn_bf16_kernel, grid, dim3(256), 0, s, p);
   else
