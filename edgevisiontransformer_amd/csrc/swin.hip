@@ -750,7 +750,8 @@ constexpr int AT96_WP = 0;                          // proj weights [96][AT96_RO
 constexpr int AT96_QKV = AT96_WP + 96 * AT96_ROW;   // 19968: window qkv [64][AT96_QROW]
 constexpr int AT96_XO = AT96_QKV + 64 * AT96_QROW;  // 57856: Xn / O / xm staging [64][AT96_ROW]
 constexpr int AT96_CV = AT96_XO + 64 * AT96_ROW;    // 71168: cqkv [288], bproj [96] (f32)
-constexpr int AT96_LDS = AT96_CV + 384 * 4;         // 72704: two blocks per CU
+constexpr int AT96_TB = AT96_CV + 384 * 4;          // 72704: compact bias tables [3][RPB_CROW]
+constexpr int AT96_LDS = AT96_TB + 3 * RPB_CROW * 4;  // 75008: two blocks per CU
 
 __global__ __launch_bounds__(256, 2) void swin_attn96_kernel(SwinAttnBlockParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -767,6 +768,21 @@ __global__ __launch_bounds__(256, 2) void swin_attn96_kernel(SwinAttnBlockParams
   }
   for (int e = tid; e < 384; e += 256)
     ((EVT_LDS float*)(L + AT96_CV))[e] = e < 288 ? p.cqkv[e] : p.bproj[e - 288];
+  {  // the three heads' compact relative-position tables (window_attn_bf16_kernel)
+    const float* cb = rpb_compact(p.bias, 3, p.shift);
+    for (int e = tid; e < 3 * RPB_CROW; e += 256) ((EVT_LDS float*)(L + AT96_TB))[e] = cb[e];
+  }
+  // per-lane table offsets b(k) of the 16 keys k = 16 kt + 4 g + j (past 48: key 48's, masked)
+  int kofs[4][4], kij[4][4];
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = min(16 * kt + 4 * g + j, 48), ki = (k * 37) >> 8;
+      kofs[kt][j] = (6 * ki + k) * 4;
+      kij[kt][j] = ki * 8 + (k - 7 * ki);  // row, column in the window
+    }
+  const int cut = 7 - p.shift;
   const int ft0 = wave * 5 - (wave > 2 ? 1 : 0), nft = wave < 2 ? 5 : 4;  // 0 / 5 / 10 / 14
   u32x4 wq[5][3];
 #pragma unroll
@@ -858,18 +874,15 @@ __global__ __launch_bounds__(256, 2) void swin_attn96_kernel(SwinAttnBlockParams
     }
     __syncthreads();
     // ---- P2: attention units (h, query tile `wave`), h = 0..2 ----
-    // bias rows of the three units first, then the next window's x prefetch: the in-order vmcnt
-    // makes every wait on a load also wait on the loads issued before it
+    // the bias from the LDS tables as in window_attn_bf16_kernel (T[a(q) - b(k)], the SW-MSA
+    // region mask and the keys past 48 as -inf); the next window's x prefetch lands during P2 / P3
     const int qt = wave;
-    f32x4 bvu[3][4];
-#pragma unroll
-    for (int h = 0; h < 3; ++h) {
-      const float* br = p.bias + ((int64_t)G.type() * 3 + h) * 49 * 64 +
-                        (int64_t)min(16 * qt + c16, 48) * 64 + 4 * g;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) bvu[h][kt] = *(const f32x4*)(br + 16 * kt);
-    }
-    if (wg + (int)gridDim.x < nwin) prefetch(wg + gridDim.x);  // lands during P2 / P3
+    if (wg + (int)gridDim.x < nwin) prefetch(wg + gridDim.x);
+    const int wtype = G.type();
+    const bool lr_ = wtype & 2, lc_ = wtype & 1;
+    const int qq = min(16 * qt + c16, 48), qi = (qq * 37) >> 8, qj = qq - 7 * qi;
+    const int toff = AT96_TB + (6 * qi + qq + 84) * 4;
+    const unsigned cq = (lr_ && qi >= cut ? 1u : 0u) | (lc_ && qj >= cut ? 2u : 0u);
     const EVT_LDS char* Q = L + AT96_QKV;
 #pragma unroll
     for (int h = 0; h < 3; ++h) {
@@ -883,29 +896,40 @@ __global__ __launch_bounds__(256, 2) void swin_attn96_kernel(SwinAttnBlockParams
                                                          f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
       }
       const f32x2 sc2 = {scale_log2, scale_log2};
+      const EVT_LDS char* Tq = L + toff + h * RPB_CROW * 4;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
-        const f32x2 lo = f32x2{sv[kt][0], sv[kt][1]} * sc2 + f32x2{bvu[h][kt][0], bvu[h][kt][1]};
-        const f32x2 hi = f32x2{sv[kt][2], sv[kt][3]} * sc2 + f32x2{bvu[h][kt][2], bvu[h][kt][3]};
+        f32x4 bv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bv[j] = *(const EVT_LDS float*)(Tq - kofs[kt][j]);
+        const f32x2 lo = f32x2{sv[kt][0], sv[kt][1]} * sc2 + f32x2{bv[0], bv[1]};
+        const f32x2 hi = f32x2{sv[kt][2], sv[kt][3]} * sc2 + f32x2{bv[2], bv[3]};
         sv[kt] = f32x4{lo[0], lo[1], hi[0], hi[1]};
-      }
-      float mx = -INFINITY;
+        if (wtype) {  // SW-MSA window on the last row / column: keys of another region
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-        mx = fmaxf(fmaxf(mx, fmaxf(sv[kt][0], sv[kt][1])), fmaxf(sv[kt][2], sv[kt][3]));
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      float sum = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float e = __builtin_amdgcn_exp2f(sv[kt][j] - mx);
-          sv[kt][j] = e;
-          sum += e;
+          for (int j = 0; j < 4; ++j) {
+            const int ki = kij[kt][j] >> 3, kj = kij[kt][j] & 7;
+            const unsigned ck = (lr_ && ki >= cut ? 1u : 0u) | (lc_ && kj >= cut ? 2u : 0u);
+            if (ck != cq) sv[kt][j] = -INFINITY;
+          }
         }
-      sum += __shfl_xor(sum, 16, 64);
-      sum += __shfl_xor(sum, 32, 64);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)  // keys 49 .. 63
+        if (4 * g + j > 0) sv[3][j] = -INFINITY;
+      float m4[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+        m4[kt] = fmaxf(fmaxf(sv[kt][0], sv[kt][1]), fmaxf(sv[kt][2], sv[kt][3]));
+      const float mx = bfly_max_16_32(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3])));
+      float p4[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sv[kt][j] = __builtin_amdgcn_exp2f(sv[kt][j] - mx);
+        p4[kt] = (sv[kt][0] + sv[kt][1]) + (sv[kt][2] + sv[kt][3]);
+      }
+      const float sum = bfly_sum_16_32((p4[0] + p4[1]) + (p4[2] + p4[3]));
       f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -926,7 +950,7 @@ __global__ __launch_bounds__(256, 2) void swin_attn96_kernel(SwinAttnBlockParams
         }
       }
       // o[dt][j] = O^T[d = 16 dt + 4 g + j][query 16 qt + c16]
-      const float inv = 1.0f / sum;
+      const float inv = __builtin_amdgcn_rcpf(sum);
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
         const f32x2 lo = f32x2{o[dt][0], o[dt][1]} * f32x2{inv, inv};
