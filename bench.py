@@ -196,9 +196,12 @@ def pmc_traffic(model: str, dtype: str, batch: int, role: str):
         d = json.load(open(f))
     except Exception:
         return None, None
-    if d.get("role") != role or d.get("batch") != batch:
+    if d.get("batch") != batch:
         return None, None
-    return d.get("traffic_bytes_per_launch"), {"file": os.path.relpath(f, REPO),
+    r = (d.get("roles") or {}).get(role) or (d if d.get("role") == role else None)
+    if r is None:
+        return None, None
+    return r.get("traffic_bytes_per_launch"), {"file": os.path.relpath(f, REPO),
                                                "commit": d.get("commit"),
                                                "collected": d.get("collected")}
 

@@ -58,22 +58,30 @@ def select(rows, rule):
     return out
 
 
-def main():
-    root, model, dtype, batch, role = sys.argv[1:6]
+def one(root, model, dtype, role):
     rule = RULES[(family(model), dtype)][role]
     f = select(rows_for(root, "FETCH_SIZE"), rule)
     w = select(rows_for(root, "WRITE_SIZE"), rule)
     assert f and len(f) == len(w), (len(f), len(w))
     fetch = 2 * 1024 * sum(float(r["Counter_Value"]) for r in f) / len(f)
     write = 1024 * sum(float(r["Counter_Value"]) for r in w) / len(w)
-    print(json.dumps({
-        "model": model, "dtype": dtype, "batch": int(batch), "role": role,
-        "kernels": sorted({r["Kernel_Name"][:120] for r in f}),
-        "launches": len(f), "fetch_bytes_corrected_per_launch": fetch,
-        "write_bytes_per_launch": write, "traffic_bytes_per_launch": fetch + write,
-        "correction": "2 x FETCH_SIZE (gfx950: 128-B requests tallied at 64 B) + WRITE_SIZE",
-        "commit": os.environ.get("COMMIT"),
-        "collected": datetime.datetime.utcnow().strftime("%Y-%m-%dT%H:%MZ")}, indent=1))
+    return {"kernels": sorted({r["Kernel_Name"][:120] for r in f}), "launches": len(f),
+            "fetch_bytes_corrected_per_launch": fetch, "write_bytes_per_launch": write,
+            "traffic_bytes_per_launch": fetch + write}
+
+
+def main():
+    """<role> may be a comma-separated list: the first role's numbers stay at the top level, every
+    role's under "roles" (bench.py looks its dominant role up there)."""
+    root, model, dtype, batch, roles = sys.argv[1:6]
+    roles = roles.split(",")
+    per = {r: one(root, model, dtype, r) for r in roles}
+    out = {"model": model, "dtype": dtype, "batch": int(batch), "role": roles[0], **per[roles[0]],
+           "roles": per,
+           "correction": "2 x FETCH_SIZE (gfx950: 128-B requests tallied at 64 B) + WRITE_SIZE",
+           "commit": os.environ.get("COMMIT"),
+           "collected": os.environ.get("COLLECTED") or datetime.datetime.utcnow().strftime("%Y-%m-%dT%H:%MZ")}
+    print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
