@@ -1055,7 +1055,15 @@ int evt_t2t_create(const evt_t2t_desc* desc, const float* const* w, int n_weight
       Performer& P = m->perf[pi];
       P.din = ts.din[pi];
       P.dpad = (int)round_up(P.din, PAD_K);
-      EVT_RC(make_dense(m, &P.kqv, w[k + 2], w[k + 3], P.din, 3 * 64, s, w[k + 0], w[k + 1]));
+      if (m->dtype == DT_BF16) {  // output columns permuted for the performers' 16-B loads
+        float *wp = nullptr, *bp = nullptr;
+        EVT_RC(dev_alloc(m, (void**)&wp, (size_t)P.din * 3 * 64 * sizeof(float)));
+        EVT_RC(dev_alloc(m, (void**)&bp, 3 * 64 * sizeof(float)));
+        EVT_HIP(kqv_permute_launch(w[k + 2], w[k + 3], P.din, wp, bp, s), "kqv permute");
+        EVT_RC(make_dense(m, &P.kqv, wp, bp, P.din, 3 * 64, s, w[k + 0], w[k + 1]));
+      } else {
+        EVT_RC(make_dense(m, &P.kqv, w[k + 2], w[k + 3], P.din, 3 * 64, s, w[k + 0], w[k + 1]));
+      }
       const float* src[9] = {w[k + 4], w[k + 5], w[k + 6], w[k + 7], w[k + 8],
                              w[k + 9], w[k + 10], w[k + 11], w[k + 12]};
       const size_t len[9] = {32 * 64, 64 * 64, 64, 64, 64, 64 * 64, 64, 64 * 64, 64};
@@ -1137,7 +1145,7 @@ int evt_t2t_forward(evt_model* m, const float* img, int B, float* logits, void* 
     ProfScope ps(m, EVT_PROF_T2T_PERFORMER, s);
     prof_work(m, perf_flops * B * t1, (double)B * t1 * (3 * 64 + 64) * es);
     EVT_HIP(performer_launch(dt, m->kqvb, 3 * 64, B, t1, P1.w, m->part, m->pout, 64, s,
-                             gather1 ? m->tstats : nullptr),
+                             gather1 ? m->tstats : nullptr, dt == DT_BF16),
             "performer1");
   }
   // iteration 2: soft_split1 (k3 s2 p1) of the [B, S/4, S/4, 64] map -> TokenPerformer (:72-77)
@@ -1181,7 +1189,8 @@ int evt_t2t_forward(evt_model* m, const float* img, int B, float* logits, void* 
   {
     ProfScope ps(m, EVT_PROF_T2T_PERFORMER, s);
     prof_work(m, perf_flops * B * t2, (double)B * t2 * (3 * 64 + 64) * es);
-    EVT_HIP(performer_launch(dt, m->kqvb, 3 * 64, B, t2, P2.w, m->part, m->pout, 64, s),
+    EVT_HIP(performer_launch(dt, m->kqvb, 3 * 64, B, t2, P2.w, m->part, m->pout, 64, s, nullptr,
+                             dt == DT_BF16),
             "performer2");
   }
   // soft_split2 -> project Dense(D) into token rows 1..P, + CLS row, + sinusoid pos (:81-86,121-125)

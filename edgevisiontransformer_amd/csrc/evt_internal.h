@@ -173,9 +173,14 @@ hipError_t unfold_launch(int dtype, int in_f32, const void* in, int B, int H, in
                          int s, int p, void* out, int ldo, float* stats, int nslots,
                          hipStream_t st);
 size_t performer_part_floats(int B, int ntok);
+// kqv_perm (bf16): the kqv columns are in the permuted order kqv_permute_launch gives the model's
+// kqv weights (t2t.hip kqv_col: 16-B row pieces per lane); false: the reference order
 hipError_t performer_launch(int dtype, const void* kqv, int64_t ldq, int B, int ntok,
                             const PerformerWeights& w, float* part, void* out, int64_t ldo,
-                            hipStream_t s, float* tstats = nullptr);
+                            hipStream_t s, float* tstats = nullptr, bool kqv_perm = false);
+// W [K][192] / bias [192] -> Wp / bp with the output columns of each 64-feature block permuted
+hipError_t kqv_permute_launch(const float* W, const float* bias, int K, float* Wp, float* bp,
+                              hipStream_t s);
 // soft split (k 3, s 2, p 1) row statistics of the R x R token map from the per-token statistics
 // performer_launch wrote (tstats: [B*R*R][2]) -> dst [rows][nslots][2] (t2t.hip)
 hipError_t unfold_stats_launch(const float* tstats, int B, int R, float* dst, int nslots,

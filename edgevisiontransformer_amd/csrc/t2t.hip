@@ -223,11 +223,38 @@ template <> __device__ __forceinline__ void tmma<float>(f32x4& acc, const f32x4&
 // kptv[n][m] += sum_t v[t][n] kp[t][m] as 8 MFMAs (n tiles x m tiles, k = the 16 tokens): v and kp
 // are written transposed ([feature][token], fp32) to the wave's LDS so that each lane reads 4
 // consecutive tokens of one feature as its operand fragment.
-template <typename T>
+// PERM (bf16 model path): the kqv GEMM's output columns are stored permuted within each 64-feature
+// block (kqv_col): lane group g's 16 features {16 c + 4 g + j} sit at columns 16 g .. 16 g + 15,
+// so a lane reads its 4 fragments of a row as two 16-B loads instead of four 8-B ones (round-4
+// counters: both performer kernels were texture-data-unit bound on the 8-B loads).
+__host__ __device__ constexpr int kqv_col(int f) { return 16 * ((f >> 2) & 3) + 4 * (f >> 4) + (f & 3); }
+
+// the lane's 4 fragments (features 16 c + 4 (lane >> 4) + j) of one 64-feature block of a row
+template <typename T, bool PERM>
+__device__ __forceinline__ void load_block(const T* rowp, bool valid, int lane, f32x4 (&f)[4]) {
+  if constexpr (PERM) {
+    u32x4 h[2] = {u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}};
+    if (valid) {
+      h[0] = *(const u32x4*)(rowp + 16 * (lane >> 4));
+      h[1] = *(const u32x4*)(rowp + 16 * (lane >> 4) + 8);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const bf16x8 v = __builtin_bit_cast(bf16x8, h[c >> 1]);
+      const int o = 4 * (c & 1);
+      f[c] = f32x4{(float)v[o], (float)v[o + 1], (float)v[o + 2], (float)v[o + 3]};
+    }
+  } else {
+    load_frags(rowp, valid, lane, f);
+  }
+}
+
+template <typename T, bool PERM = false>
 __global__ __launch_bounds__(256) void performer_kv_kernel(const T* __restrict__ kqv, int64_t ldq,
                                                            int ntok, int chunk,
                                                            const float* __restrict__ prmw,
                                                            float* __restrict__ part) {
+  static_assert(!PERM || std::is_same<T, bf16>::value, "permuted kqv: bf16 path");
   constexpr int TS = 20;  // floats per transposed row (16 tokens + 4 pad: conflict-light writes)
   constexpr int TILES = 4 * (PF_HS + PF_M) * TS;
   __shared__ __attribute__((aligned(16))) float smem[PF_M * 64 + (TILES > 4 * PF_PART ? TILES : 4 * PF_PART)];
@@ -256,8 +283,8 @@ __global__ __launch_bounds__(256) void performer_kv_kernel(const T* __restrict__
     const bool valid = t < t_hi;
     const T* rowp = kqv + ((int64_t)b * ntok + t) * ldq;
     f32x4 kf[4], vf[4];
-    load_frags(rowp, valid, lane, kf);              // k = columns [0, 64)   (split order k, q, v)
-    load_frags(rowp + 2 * PF_HS, valid, lane, vf);  // v = columns [128, 192)
+    load_block<T, PERM>(rowp, valid, lane, kf);              // k = columns [0, 64) (split order k, q, v)
+    load_block<T, PERM>(rowp + 2 * PF_HS, valid, lane, vf);  // v = columns [128, 192)
     float kd = 0.f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) kd += kf[c][0] * kf[c][0] + kf[c][1] * kf[c][1] + kf[c][2] * kf[c][2] + kf[c][3] * kf[c][3];
@@ -466,6 +493,7 @@ __device__ __forceinline__ Afrag<bf16> po_frag(const EVT_LDS bf16* M, int cols, 
   return f;
 }
 
+template <bool PERM>
 __global__ __launch_bounds__(256, 4) void performer_out16_kernel(const bf16* __restrict__ kqv,
                                                                 int64_t ldq, int ntok, int span,
                                                                 const float* __restrict__ part,
@@ -503,15 +531,28 @@ __global__ __launch_bounds__(256, 4) void performer_out16_kernel(const bf16* __r
   const float inv_sqrt_m = 1.0f / sqrtf((float)PF_M);
   const int t_lo = blockIdx.x * span, t_hi = min(ntok, t_lo + span);
   const int g4 = 4 * (lane >> 4);
-  // raw bf16 q / v of a tile: 4 + 4 pieces of 4 features (8 B each)
+  // raw bf16 q / v of a tile: 4 + 4 pieces of 4 features (8 B each; PERM: two 16-B loads per
+  // block, kqv_col)
   auto load_raw = [&](int t0, u32x2 (&r)[8]) {
     const int t = t0 + (lane & 15);
     const bool valid = t < t_hi;
     const bf16* rowp = kqv + ((int64_t)b * ntok + (valid ? t : t_lo)) * ldq;
+    if constexpr (PERM) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      r[c] = *(const u32x2*)(rowp + PF_HS + 16 * c + g4);
-      r[4 + c] = *(const u32x2*)(rowp + 2 * PF_HS + 16 * c + g4);
+      for (int blk = 0; blk < 2; ++blk) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const u32x4 v = *(const u32x4*)(rowp + (1 + blk) * PF_HS + 16 * (lane >> 4) + 8 * hh);
+          r[4 * blk + 2 * hh] = u32x2{v[0], v[1]};
+          r[4 * blk + 2 * hh + 1] = u32x2{v[2], v[3]};
+        }
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        r[c] = *(const u32x2*)(rowp + PF_HS + 16 * c + g4);
+        r[4 + c] = *(const u32x2*)(rowp + 2 * PF_HS + 16 * c + g4);
+      }
     }
   };
   auto f4 = [](u32x2 v) {
@@ -772,12 +813,12 @@ __global__ __launch_bounds__(256) void performer_reduce_kernel(const float* __re
   fin[(int64_t)b * PF_PART + i] = v;
 }
 
-template <typename T>
+template <typename T, bool PERM = false>
 hipError_t performer_t(const void* kqv, int64_t ldq, int B, int ntok, int chunk, int nchunk,
                        float* part, const PerformerWeights& w, int span, void* out, int64_t ldo,
                        hipStream_t s, float* tstats) {
-  hipLaunchKernelGGL(performer_kv_kernel<T>, dim3(nchunk, B), dim3(256), 0, s, (const T*)kqv, ldq,
-                     ntok, chunk, w.prmw, part);
+  hipLaunchKernelGGL((performer_kv_kernel<T, PERM>), dim3(nchunk, B), dim3(256), 0, s,
+                     (const T*)kqv, ldq, ntok, chunk, w.prmw, part);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   // the chunk partials summed once per image (the output workgroups then read one partial each)
@@ -785,7 +826,7 @@ hipError_t performer_t(const void* kqv, int64_t ldq, int B, int ntok, int chunk,
   hipLaunchKernelGGL(performer_reduce_kernel, dim3((PF_PART + 255) / 256, B), dim3(256), 0, s,
                      part, nchunk, fin);
   if constexpr (std::is_same<T, bf16>::value) {
-    hipLaunchKernelGGL(performer_out16_kernel, dim3((ntok + span - 1) / span, B), dim3(256),
+    hipLaunchKernelGGL(performer_out16_kernel<PERM>, dim3((ntok + span - 1) / span, B), dim3(256),
                        PF_OUT16_LDS, s, (const bf16*)kqv, ldq, ntok, span, fin, w, (bf16*)out, ldo,
                        tstats);
     return hipGetLastError();
@@ -820,17 +861,37 @@ size_t performer_part_floats(int B, int ntok) {
 
 hipError_t performer_launch(int dtype, const void* kqv, int64_t ldq, int B, int ntok,
                             const PerformerWeights& w, float* part, void* out, int64_t ldo,
-                            hipStream_t s, float* tstats) {
+                            hipStream_t s, float* tstats, bool kqv_perm) {
   if (B <= 0 || ntok <= 0) return hipSuccess;
   if (ldq < 3 * PF_HS || ldo < PF_HS || (ldq & 3) || (ldo & 3)) return hipErrorInvalidValue;
-  if (tstats && dtype != DT_BF16) return hipErrorInvalidValue;
+  if ((tstats || kqv_perm) && dtype != DT_BF16) return hipErrorInvalidValue;
+  if (kqv_perm && (ldq & 7)) return hipErrorInvalidValue;  // 16-B row pieces
   const int nchunk = performer_chunks(ntok);
   const int chunk = (ntok + nchunk - 1) / nchunk;
   const int span = 512;  // tokens per output workgroup
-  return dtype == DT_BF16
-             ? performer_t<bf16>(kqv, ldq, B, ntok, chunk, nchunk, part, w, span, out, ldo, s, tstats)
-             : performer_t<float>(kqv, ldq, B, ntok, chunk, nchunk, part, w, span, out, ldo, s,
-                                  nullptr);
+  if (dtype != DT_BF16)
+    return performer_t<float>(kqv, ldq, B, ntok, chunk, nchunk, part, w, span, out, ldo, s, nullptr);
+  return kqv_perm
+             ? performer_t<bf16, true>(kqv, ldq, B, ntok, chunk, nchunk, part, w, span, out, ldo, s,
+                                       tstats)
+             : performer_t<bf16>(kqv, ldq, B, ntok, chunk, nchunk, part, w, span, out, ldo, s, tstats);
+}
+
+// the model's kqv weight / bias with the output columns in kqv_col order within each 64 block
+__global__ void kqv_permute_kernel(const float* __restrict__ W, const float* __restrict__ bias,
+                                   int K, float* __restrict__ Wp, float* __restrict__ bp) {
+  const int e = blockIdx.x * 256 + threadIdx.x;  // over (K + 1) x 192
+  if (e >= (K + 1) * 3 * PF_HS) return;
+  const int k = e / (3 * PF_HS), n = e - k * 3 * PF_HS, blk = n / PF_HS, f = n - blk * PF_HS;
+  const int dst = blk * PF_HS + kqv_col(f);
+  if (k < K) Wp[(int64_t)k * 3 * PF_HS + dst] = W[(int64_t)k * 3 * PF_HS + n];
+  else bp[dst] = bias[n];
+}
+hipError_t kqv_permute_launch(const float* W, const float* bias, int K, float* Wp, float* bp,
+                              hipStream_t s) {
+  const int n = (K + 1) * 3 * PF_HS;
+  hipLaunchKernelGGL(kqv_permute_kernel, dim3((n + 255) / 256), dim3(256), 0, s, W, bias, K, Wp, bp);
+  return hipGetLastError();
 }
 
 // Statistics of the soft split (k 3, s 2, p 1) rows from per-token statistics: row (b, y, x) of
