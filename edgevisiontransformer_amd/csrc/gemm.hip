@@ -2126,12 +2126,18 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     stamp(2);
-    // producer: every wave passed this tile's K-tile-1 waits (vmcnt <= 8 with more than 8 younger
-    // DMAs; vmcnt counts loads, stores, atomics and LDS-DMA together in issue order,
-    // MI355X_MICROARCH.md) before the barriers wave 0 has crossed since: the previous tile's
-    // write-through stores and statistics are complete
+    // producer: the previous tile's write-through stores and statistics must be complete in every
+    // wave before thread 0 publishes its panel. The counted K-tile-1 waits already imply it where
+    // vmcnt retires loads, stores and LDS-DMA in issue order (MI355X_MICROARCH.md); the compiler's
+    // model does not assume that ordering, so every wave also drains its vector-memory
+    // counter and the block meets at a barrier first. This drains the next tile's prologue DMAs
+    // once per tile: a cost on the opt-in chained path only (the separate launches publish nothing).
     if constexpr ((ROLE & 1) != 0) {
-      if (pub_tm >= 0 && tid == 0) chain_publish(smem, pub_tm);
+      if (pub_tm >= 0) {
+        wait_vmcnt0();
+        big8_bar();
+        if (tid == 0) chain_publish(smem, pub_tm);
+      }
       pub_tm = tm;
     }
     const bool interior = (m0 + BIG_BM <= p.M) && (n0 + BIG_BN <= p.N);
