@@ -578,8 +578,8 @@ __global__ __launch_bounds__(256) void ln_pool_kernel(const T* __restrict__ x, i
 // here it is xm in + x out (0.3 GB) and each SIMD runs two waves whose MFMA and VALU phases
 // interleave.
 //   LDS (whole block, loaded once): W1 = the LN2-folded FC1 weights, 384 hidden rows x 96 k
-//   (208-B rows: the 16 lanes of one k chunk hit distinct 4-bank groups), and W2 = FC2, 96 output
-//   rows x 384 hidden (784-B rows) with the hidden axis permuted per 32-chunk so that the FC1
+//   (224-B rows), and W2 = FC2, 96 output
+//   rows x 384 hidden (800-B rows) with the hidden axis permuted per 32-chunk so that the FC1
 //   accumulators ARE the FC2 B operand: chunk position 8g + s holds hidden 4g + s (s < 4) or
 //   16 + 4g + (s - 4) - the two 16-row FC1 tiles of the chunk, as lane group g holds them.
 //   Wave = 32 tokens (2 tiles of 16), their rows normalised once in registers ((x - mu) r; gamma
@@ -588,8 +588,11 @@ __global__ __launch_bounds__(256) void ln_pool_kernel(const T* __restrict__ x, i
 //   Products are transposed (C^T = A . B) so one token is one lane column throughout. The
 //   per-lane VALU work (GELU) is the bound: erf GELU in its fast bf16-path form.
 constexpr int MLP96_C = 96, MLP96_F = 384;
-constexpr int MLP96_W1_ROW = 208, MLP96_W2_ROW = 784;
-constexpr int MLP96_LDS = MLP96_F * MLP96_W1_ROW + MLP96_C * MLP96_W2_ROW;  // 155136 B
+// row pitches from scripts/probe/lds_conflicts.py's lane-group model: 208 / 784 put two 16-B
+// reads on one bank group in half of the W1 and W2 fragment reads (measured round 4: 48 % of the
+// LDS-active cycles were bank conflicts); 224 / 800 have none (162816 B of the 163840)
+constexpr int MLP96_W1_ROW = 224, MLP96_W2_ROW = 800;
+constexpr int MLP96_LDS = MLP96_F * MLP96_W1_ROW + MLP96_C * MLP96_W2_ROW;  // 162816 B
 // 12 waves (3 per SIMD, <= 168 VGPRs): the MFMA -> GELU -> MFMA chain of one wave leaves the
 // SIMD idle on latencies that a third wave fills
 constexpr int MLP96_WAVES = 12;
