@@ -64,6 +64,13 @@ __device__ __forceinline__ void buffer_store_b128(u32x4 v, __amdgpu_buffer_rsrc_
   __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, AUX);
   wide_store_fence();
 }
+// 64-bit buffer store: outside the hazard class above (data of at most 64 bits), no fence; a
+// helper so that the source check of tests/test_isa_hazards.py still sees every raw buffer store
+template <int AUX>
+__device__ __forceinline__ void buffer_store_b64(u32x2 v, __amdgpu_buffer_rsrc_t rs, int voff,
+                                                 int soff) {
+  __builtin_amdgcn_raw_buffer_store_b64(v, rs, voff, soff, AUX);
+}
 __device__ __forceinline__ void store_f32x4(float* p, f32x4 v) {
   store_b128(p, __builtin_bit_cast(u32x4, v));
 }

@@ -469,11 +469,11 @@ __global__ __launch_bounds__(256) void window_attn_bf16_kernel(SwinAttnParams p)
       for (int dt = 0; dt < 2; ++dt) {
         const f32x4 v = o[dt] * inv;
         const bf16x4 ob = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, ob), ro, qoff[qt], 32 * dt, 0);
+        buffer_store_b64<0>(__builtin_bit_cast(u32x2, ob), ro, qoff[qt], 32 * dt);
       }
       if (h == 0)  // pad columns [C, ldo) of the attention output (the proj GEMM's K padding)
         for (int c = p.C + 4 * g; c < p.ldo; c += 16)
-          __builtin_amdgcn_raw_buffer_store_b64(u32x2{0u, 0u}, ro, qoff[qt] + (c - 4 * g) * 2, 0, 0);
+          buffer_store_b64<0>(u32x2{0u, 0u}, ro, qoff[qt] + (c - 4 * g) * 2, 0);
     }
   }
 }
