@@ -1656,7 +1656,7 @@ int evt_diag_occupy(int blocks, int usec, void* stream) {
 
 int evt_set_gemm_variant(int variant) {
   if (!gemm_variant_supported(variant))
-    return fail(EVT_EINVAL, "variant must be 0, 1, 2, 6, 8, 9, 16, 30, 31 or 32 (lab builds: also "
+    return fail(EVT_EINVAL, "variant must be 0, 1, 2, 6, 8, 9, 16, 30, 31, 32, 34 or 35 (lab builds: also "
                             "10, 11, 13, 15, 17-25, 106, 108)");
   gemm_set_variant(variant);
   return EVT_OK;

@@ -56,6 +56,8 @@ struct GemmParams {
   float* sk_part;                     // stream-K partial tiles [#CUs][256 * 256] fp32
   int ks_chunk;                       // split-K (128x128 kernel, gridDim.y splits): K per split;
   int64_t ks_stride;                  // fp32 partial C of split z at C + z * ks_stride
+  int xgroups;                        // persistent 256x256 walk: XCD groups that each own
+                                      // ntiles / xgroups weight panels (0 / 1: one group)
 };
 constexpr int GEMM_BM = 128;
 constexpr int GEMM_BN = 128;
@@ -270,7 +272,8 @@ int gemm_variant();  // the calling thread's evt_set_gemm_variant value (0 = aut
 // automatic kernel selection (0; 30 / 31 only steer the 128 x 384 tiles): fused kernels allowed
 inline bool gemm_auto() {
   const int v = gemm_variant();
-  return v == 0 || v == 30 || v == 31 || v == 32 || v == 33;  // (33: EVT_RIA lab builds)
+  return v == 0 || v == 30 || v == 31 || v == 32 || v == 33 || v == 34 ||
+         v == 35;  // (33: EVT_RIA lab builds; 34 / 35: XCD groups of the persistent walk)
 }
 bool gemm_variant_supported(int v);  // compiled into this build (lab variants: EVT_GEMM_LAB)
 

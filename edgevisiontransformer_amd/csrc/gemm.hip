@@ -509,8 +509,9 @@ bool use_big(const GemmParams& p, int flags) {
   if ((p.ntiles * GEMM_BN) % BIG_BN) return false;
   if (!(flags & EPI_OUT_F32) && p.vec_ok < 2) return false;  // big epilogue: 16-B bf16 stores only
   // 31: automatic without 128 x 384; 32: automatic with the round-3 rule (>= 256 big tiles)
-  const int v = (g_gemm_variant == 31 || g_gemm_variant == 32 || g_gemm_variant == 33)
-                    ? 0 : g_gemm_variant;  // (33: EVT_RIA lab builds)
+  const int v = (g_gemm_variant == 31 || g_gemm_variant == 32 || g_gemm_variant == 33 ||
+                 g_gemm_variant == 34 || g_gemm_variant == 35)
+                    ? 0 : g_gemm_variant;  // (33: EVT_RIA lab builds; 34 / 35: XCD groups)
   if (v == 1) return false;
   if (v >= 2) return true;
   // 256x256 tiles unless their rounds cost more: time in 256-tile units, the 128x128 kernel at a
@@ -1987,6 +1988,31 @@ __device__ __forceinline__ void chain_wait(ChainCtx& cx, int tm, char* smem) {
   cx.all_ready = __builtin_amdgcn_readfirstlane(*(const EVT_LDS int*)(smem + CHAIN_WORD)) != 0;
 }
 
+// Logical walk index -> output tile of the persistent 256 x 256 kernel. Walk index t of round
+// r = t / G runs on XCD x of its round slot (blocks b and b + 8 share an XCD; the start index of
+// block b is x (G / 8) + (b >> 3), x = b & 7). One group (xgroups <= 1): the rounds sweep the tiles
+// m-panel-major, so an XCD's 32 tiles of a round span every weight panel of a wide GEMM (FC1: all
+// 12, 4.7 MB, more than its 4 MB L2, fetched again from beyond L2 every round). xgroups = g: the
+// XCDs form g groups of 8 / g, group k owns weight panels [k ntiles / g, (k + 1) ntiles / g) for
+// the whole launch and walks the m-panels of that slice in the same m-major order, so the slice
+// (FC1, g = 2: 2.4 MB) can stay in its XCDs' L2 across rounds while the A panels stream (each A
+// panel then read by g XCD groups). Returns whether t names a tile. Which tile a block runs never
+// changes a tile's arithmetic (bitwise the same outputs for every xgroups).
+__device__ __forceinline__ bool pers_tile(int t, int G, int ntiles, int xgroups, int total, int& tm,
+                                          int& tn) {
+  if (xgroups <= 1) {
+    tm = t / ntiles;
+    tn = t - tm * ntiles;
+    return t < total;
+  }
+  const int q = G >> 3, r = t / G, w = t - r * G, x = w / q, l = w - x * q;
+  const int xs = 8 / xgroups, k = x / xs, j = (r * xs + (x - k * xs)) * q + l;
+  const int ntg = ntiles / xgroups;
+  tm = j / ntg;
+  tn = k * ntg + (j - tm * ntg);
+  return j < total / xgroups;
+}
+
 // The persistent tile walk of one GEMM from logical tile `tile`: in steps of gridDim.x (ROLE 0, a
 // plain launch), or the block's dequeued walk indices (chained launch, ChainCtx): ROLE bit 1 =
 // producer (outputs write-through; a tile's panel is published at the block's next epilogue,
@@ -2009,7 +2035,9 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
   const int wm = wave >> 2, wn = wave & 3;
   const int G = gridDim.x;
   const int nk = p.K / 64;
-  int tm = tile / p.ntiles, tn = tile - tm * p.ntiles;
+  const int xg = ROLE == 0 ? p.xgroups : 0;
+  int tm, tn;
+  pers_tile(tile, G, p.ntiles, xg, total, tm, tn);
   if (DBG == 5) {  // experiment: stagger the blocks' start
     const int q = (blockIdx.x >> 3) & 3;
     for (int i = 0; i < q * nk; ++i) __builtin_amdgcn_s_sleep(20);
@@ -2044,12 +2072,9 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
     asm volatile("" : "+v"(ln));  // per-tile lane addresses: not hoisted out of the tile loop
     u32x4 rre[2][4];  // ER: residual row pair 0 loaded before the last K-tile
     const int next = ROLE == 0 ? tile + G : cx.nxt - cx.base;
-    const bool has_next = next >= 0 && next < total;
     int ntm = 0, ntn = 0;
-    if (has_next) {
-      ntm = next / p.ntiles;
-      ntn = next - ntm * p.ntiles;
-    }
+    const bool has_next = next >= 0 && pers_tile(next, G, p.ntiles, xg, total, ntm, ntn);
+    if (!has_next) ntm = ntn = 0;
     // consumer: the next tile's operands may be fetched ahead only once every panel is known ready
     const bool rdy = !WAITS || cx.all_ready;
     // the next tile's prologue rides in the last K-tiles' idle DMA slots (big8_ktile) as K-tiles
@@ -2174,7 +2199,10 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
   __shared__ __attribute__((aligned(16))) char smem[PERS_LDS_ALL];
   const int G = gridDim.x;  // XCD-aware order when a multiple of 8
   const int tile = (G & 7) ? (int)blockIdx.x : (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
-  if (tile >= total) return;
+  {
+    int tm, tn;
+    if (!pers_tile(tile, G, p.ntiles, p.xgroups, total, tm, tn)) return;
+  }
   ChainCtx cx;
   if constexpr ((FL & EPI_GATHER) != 0) {
     MergeParams q;
@@ -2815,7 +2843,8 @@ bool gemm_lab_pers_variant(int v) {
 
 bool use_pers(const GemmParams& p, int flags) {
   const int v = g_gemm_variant;
-  if (v != 0 && v != 9 && v != 16 && v != 31 && v != 32 && v != 33 && !gemm_lab_pers_variant(v))
+  if (v != 0 && v != 9 && v != 16 && v != 31 && v != 32 && v != 33 && v != 34 && v != 35 &&
+      !gemm_lab_pers_variant(v))
     return false;
   // timeline variants stamp s_memtime through p.pos: never on the patch GEMM (p.pos = the table)
   if ((v == 13 || v == 15) && (flags & EPI_POS)) return false;
@@ -2845,6 +2874,15 @@ bool launch_pers_ria(const GemmParams& q, int G, int total, hipStream_t s) {
   }
 }
 
+// XCD groups of the persistent walk (pers_tile): 2 where the weight panels split evenly over
+// two groups of four XCDs and the launch has more than one round (FC1 of the D = 768 models: 12
+// panels -> 6 per group); variant 34 keeps one group, 35 asks for 4 (A/B)
+int pers_xgroups(int ntiles, int G, int total) {
+  if (G != 256 || total <= G) return 1;  // the walk arithmetic assumes 8 XCDs of 32 blocks
+  const int want = g_gemm_variant == 34 ? 1 : g_gemm_variant == 35 ? 4 : 2;
+  return (ntiles % want == 0 && ntiles / want >= 3) ? want : 1;
+}
+
 template <int FL>
 hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
   num_cus();
@@ -2853,6 +2891,7 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
   const int total = ((p.M + BIG_BM - 1) / BIG_BM) * q.ntiles;
   int G = min(total, g_gemm_variant == 10 ? 8 : g_num_cus);  // 10: few blocks, many tiles each
   if (G >= 8 && total > G) G &= ~7;  // (one round: one block per tile, no rounding down)
+  q.xgroups = pers_xgroups(q.ntiles, G, total);
   if (false) {
   }
 #ifdef EVT_GEMM_LAB
@@ -3125,7 +3164,7 @@ int device_cus() { return num_cus(); }
 void gemm_set_variant(int v) { g_gemm_variant = v; }
 bool gemm_variant_supported(int v) {
   return v == 0 || v == 1 || v == 2 || v == 6 || v == 8 || v == 9 || v == 16 || v == 30 || v == 31 ||
-         v == 32 || (EVT_RIA && v == 33) ||
+         v == 32 || (EVT_RIA && v == 33) || v == 34 || v == 35 ||
          gemm_lab_pers_variant(v)
 #ifdef EVT_GEMM_LAB
          || v == 106 || v == 108

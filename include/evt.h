@@ -465,7 +465,9 @@ int evt_attention_mx8(const void* qkv, int64_t ldq, void* q8, int64_t ldq8, uint
  * tiles with the plain / interleaved / 8-phase ping-pong main loop whenever the packed width
  * allows, 9 = tile-persistent, 16 = stream-K persistent where it applies, 30 = the 128 x 384
  * persistent tiles wherever the width allows (multiple of 384), 31 = automatic without them, 32 =
- * automatic with the round-3 tile rule (256 x 256 tiles only from 256 of them up). Builds with
+ * automatic with the round-3 tile rule (256 x 256 tiles only from 256 of them up), 34 / 35 =
+ * automatic with the persistent walk's weight panels split over 1 / 4 XCD groups (the default
+ * splits them over 2 where they divide evenly; outputs are bitwise the same). Builds with
  * EVT_LAB=1 (-DEVT_GEMM_LAB) also accept the ablation / timeline variants 10, 11, 13, 15, 17-25,
  * 106, 108; other values return EVT_EINVAL. */
 int evt_set_gemm_variant(int variant);

@@ -63,7 +63,7 @@ def test_host_validation_codes(lib):
     assert lib.evt_model_set_fusion(None, 0) == _lib.EVT_EINVAL
     assert lib.evt_set_gemm_variant(20) == _lib.EVT_EINVAL  # lab-only ablation (product build)
     assert b"lab builds" in lib.evt_last_error()
-    for v in (1, 2, 6, 8, 9, 16, 30, 31, 32, 0):
+    for v in (1, 2, 6, 8, 9, 16, 30, 31, 32, 34, 35, 0):
         assert lib.evt_set_gemm_variant(v) == 0
     assert lib.evt_graph_launch(None, None) == _lib.EVT_EINVAL
     assert lib.evt_graph_capture(None, None, 1, None, None) == _lib.EVT_EINVAL
