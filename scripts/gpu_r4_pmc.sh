@@ -24,6 +24,6 @@ deit_base fc1 --model deit_base --dtype bf16 --batch 512
 t2t_vit_14 fc1 --model t2t_vit_14 --dtype bf16 --batch 256
 swin_tiny fc2 --model swin_tiny --dtype bf16 --batch 256
 deit_tiny_f32 fc2 --model deit_tiny --dtype f32 --batch 256
-deit_base_bs64 fc2 --model deit_base --dtype bf16 --batch 64
+deit_base_bs64 fc1 --model deit_base --dtype bf16 --batch 64
 L
 if [ -n "${SQ:-}" ]; then TAG=_r4 bash $R/scripts/gpu_pmc_sq.sh > $O/sq.log 2>&1 || exit 1; tail -40 $O/sq.log; fi
