@@ -52,7 +52,7 @@ sys.path.insert(0, REPO)
 PEAK_BF16_TFLOPS = 2516.6   # MI355X dense bf16 MFMA (spec; MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3     # MI355X fp32 matrix (spec)
 PEAK_HBM_GBPS = 8000.0      # MI355X HBM3E (spec; MI355X_MICROARCH.md)
-PMC_DIR = os.path.join(REPO, "profiles")  # pmc_<model>_<dtype>_bs<batch>.json (scripts/gpu_r4_pmc.sh)
+PMC_DIR = os.path.join(REPO, "profiles")  # pmc_<model>_<dtype>_bs<batch>.json (scripts/gpu_run.sh pmc:<name>:<role>:<args>)
 def kernel_label(model: str, dtype: str, role: str) -> str:
     """The kernels a role's launches run (persistent 256x256 GEMM where the tile count fills the
     chip, else the 128x128 one; the fp32 path always the latter)."""
@@ -85,10 +85,6 @@ def parse():
     ap.add_argument("--gemm-variant", type=int, default=0, help="evt_set_gemm_variant (tuning A/B)")
     ap.add_argument("--isolated-probe", action="store_true",
                     help="also time FC1 alone, back to back (reported as roofline.isolated_probe_us)")
-    ap.add_argument("--fusion", type=int, default=-1,
-                    help="evt_model_set_fusion flags (-1 = the library default 0: separate "
-                         "kernels; 2 = chained out-proj -> FC1 GEMM launches; 1 = fused QKV + "
-                         "attention)")
     ap.add_argument("--probe-only", type=int, default=0, metavar="N",
                     help="only launch the FC1 probe kernel N times and exit (PMC collection)")
     ap.add_argument("--global-batch", type=int, default=0,
@@ -188,7 +184,7 @@ def cpu_baseline(model_name: str, budget_s: float) -> dict:
 def pmc_traffic(model: str, dtype: str, batch: int, role: str):
     """HBM bytes per launch of `role`'s kernels in real forwards of this configuration, from the
     rocprofv3 PMC passes committed as profiles/pmc_<model>_<dtype>_bs<batch>.json
-    (scripts/gpu_r4_pmc.sh + scripts/pmc_roles.py: 2 x FETCH_SIZE, gfx950 tallies 128-B requests
+    (scripts/gpu_run.sh pmc + scripts/pmc_roles.py: 2 x FETCH_SIZE, gfx950 tallies 128-B requests
     at 64 B, MI355X_MICROARCH.md HBM section, + WRITE_SIZE, averaged over the role's launches) and
     the build commit it measured. None if absent or collected for another role."""
     f = os.path.join(PMC_DIR, f"pmc_{model}_{dtype}_bs{batch}.json")
@@ -243,10 +239,6 @@ def main():
     else:
         B, G, cap = args.batch, world * args.batch, args.batch
     model = mod.build_named(args.model, dtype=args.dtype, seed=0, max_batch=cap)
-    if args.fusion >= 0:
-        if not hasattr(model, "set_fusion"):  # the fusion switches are ViT / T2T-ViT ones
-            raise SystemExit(f"--fusion does not apply to {args.model}")
-        model.set_fusion(args.fusion)
     if args.gemm_variant:
         from edgevisiontransformer_amd import _lib
         _lib.check(_lib.load_library().evt_set_gemm_variant(args.gemm_variant))
@@ -346,8 +338,7 @@ def main():
                        "model": args.model, "global_batch": G, "per_gpu_batch": cap,
                        "seq_len": model.cfg.res(0) ** 2 if swin else model.cfg.tokens,
                        "parallelism": par,
-                       "fusion": "library default (separate kernels)" if args.fusion < 0
-                                 else args.fusion},
+                       "gemm_variant": args.gemm_variant or "automatic"},
             "model_roofline": {"achieved_tflops": round(imgs_per_s * gflop_img / world / 1e3, 2),
                                "peak": peak, "frac": round(imgs_per_s * gflop_img / world / 1e3
                                                            / peak, 4),

@@ -27,11 +27,9 @@ DTYPE = {"f32": 0, "fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1, "mx8": 2}
 EPI_BIAS, EPI_GELU, EPI_RESID, EPI_POS, EPI_OUT_F32 = 1, 2, 4, 8, 16
 EPI_LNIN, EPI_RESLN, EPI_STATS, EPI_GELU_ERF = 32, 64, 128, 256
 EPI_OUT_MX8 = 512
-FUSE_QKV_ATTENTION = 1  # evt_model_set_fusion flag (include/evt.h EVT_FUSE_QKV_ATTENTION)
-FUSE_GEMM_CHAIN = 2  # evt_model_set_fusion flag (EVT_FUSE_GEMM_CHAIN: out-proj -> FC1, opt-in)
 # evt_model_profile roles (include/evt.h EVT_PROF_*)
 PROF_ROLES = ("patchify", "patch_embed", "qkv", "attention", "out_proj", "fc1", "fc2", "head",
-              "qkv_attention", "t2t_unfold", "t2t_kqv", "t2t_performer", "merge", "attn_sublayer",
+              "(unused)", "t2t_unfold", "t2t_kqv", "t2t_performer", "merge", "attn_sublayer",
               "mlp")
 SWIN_MAX_STAGES = 8
 
@@ -113,14 +111,9 @@ SIGNATURES = {
     "evt_graph_capture": (_I, [_P, _P, _I, _P, _P]),
     "evt_graph_launch": (_I, [_P, _P]),
     "evt_set_gemm_variant": (_I, [_I]),
-    "evt_model_set_fusion": (_I, [_P, _I]),
-    "evt_model_status": (_I, [_P]),
-    "evt_model_set_chain_spin": (_I, [_P, _I64]),
-    "evt_diag_occupy": (_I, [_I, _I, _P]),
     "evt_model_profile": (_I, [_P, _I]),
     "evt_model_profile_read": (_I, [_P, _P, _P]),
     "evt_model_profile_work": (_I, [_P, _P, _P]),
-    "evt_qkv_attention": (_I, [_P, _I, _P, _P, _P, _P, _I, _I, _I, _F, _F, _P, _I64, _P]),
     "evt_pack_weight": (_I, [_I, _P, _P, _I, _I, _P, _I, _I, _P]),
     "evt_ln_fold": (_I, [_I, _P, _I, _I, _P, _P, _P, _I, _I, _P, _P, _P]),
     "evt_dense": (_I, [_I, ctypes.POINTER(evt_dense_args), _P]),
@@ -170,7 +163,13 @@ def load_library() -> ctypes.CDLL:
                     f"{LIB_PATH} not found: build it with `python -m edgevisiontransformer_amd.build`"
                     " (hipcc --offload-arch=gfx950). There is no CPU fallback.")
             lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+            # an EVT_LIB override (a lab build, or an older build for an A/B measurement) may lack
+            # entry points added since: those stay unbound there; the in-tree library must export
+            # every one (tests/test_capi.py)
+            lenient = "EVT_LIB" in os.environ
             for name, (res, args) in SIGNATURES.items():
+                if lenient and not hasattr(lib, name):
+                    continue
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args
@@ -201,10 +200,3 @@ def ensure_device(device_index: int) -> None:
 
 def stream_ptr(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
-
-
-def diag_occupy(blocks: int, usec: int, stream: int) -> None:
-    """Diagnostics (evt_diag_occupy): `blocks` workgroups holding one CU each for `usec` us on
-    `stream` (a torch stream's cuda_stream handle): another stream's load for the chained-launch
-    tests."""
-    check(load_library().evt_diag_occupy(int(blocks), int(usec), ctypes.c_void_p(stream)))

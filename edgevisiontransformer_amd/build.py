@@ -17,7 +17,7 @@ CSRC = os.path.join(HERE, "csrc")
 LAB = os.environ.get("EVT_LAB", "") not in ("", "0")
 LIB = os.path.join(HERE, "libevt_hip_lab.so" if LAB else "libevt_hip.so")
 OBJ = os.path.join(HERE, "build_obj_lab" if LAB else "build_obj")
-SOURCES = ["gemm.hip", "attention.hip", "qkv_attn.hip", "norm.hip", "t2t.hip", "swin.hip", "mx8.hip", "capi.cpp"]
+SOURCES = ["gemm.hip", "attention.hip", "norm.hip", "t2t.hip", "swin.hip", "mx8.hip", "capi.cpp"]
 HEADERS = ["common.h", "evt_internal.h", os.path.join("..", "..", "include", "evt.h")]
 ARCH = os.environ.get("EVT_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
@@ -37,9 +37,6 @@ PER_FILE_FLAGS = {s: ["-mllvm", "-amdgpu-mfma-vgpr-form=true"]
 # attention.hip: no NaN operands either (scores of finite bf16 / fp32 q, k; masked keys are -inf):
 # the softmax max runs on the raw MFMA results without a canonicalising v_max per element
 PER_FILE_FLAGS["attention.hip"] = PER_FILE_FLAGS["attention.hip"] + ["-fno-honor-nans"]
-# qkv_attn.hip: no NaN operands on the path, so fmaxf on raw MFMA results needs no canonicalising
-# v_max per element before the softmax max tree (-inf masking is unaffected)
-PER_FILE_FLAGS["qkv_attn.hip"] = ["-fno-honor-nans"]
 # swin.hip: the same for the window-attention softmax (finite scores, -inf masks; 32 canonicalising
 # v_max per wave before, round-4 counters)
 PER_FILE_FLAGS["swin.hip"] = PER_FILE_FLAGS["swin.hip"] + ["-fno-honor-nans"]

@@ -146,9 +146,6 @@ struct evt_model {
   size_t hbuf_bytes = 0;
   void* hh = nullptr;        // [B, head_st]
   void* sk = nullptr;        // stream-K scratch of the model's GEMMs (gemm_sk_bytes)
-  ChainWords chain;          // hand-off words of chained GEMM launches (gemm_chain_launch)
-  unsigned* status = nullptr; // host-mapped status word (chain.err is its device view): set by a
-                              // chained launch whose bounded hand-off wait gave up
   // Swin (family 2)
   evt_swin_desc sdesc{};
   std::vector<SwinStage> stages;
@@ -158,7 +155,6 @@ struct evt_model {
   hipGraph_t graph = nullptr;        // evt_graph_capture
   hipGraphExec_t graph_exec = nullptr;
   // evt_model_profile: HIP events around every launch of the last forward, by role
-  int fusion = 0;                    // evt_model_set_fusion
   bool prof = false;
   std::vector<hipEvent_t> prof_ev;   // pool (pairs)
   std::vector<int> prof_role;        // role of pair i of the last forward
@@ -434,21 +430,6 @@ int dense(const evt_model* m, const DenseW& w, const DenseCall& c, hipStream_t s
   return EVT_OK;
 }
 
-// Producer Dense (out-proj) and the consumer Dense reading its output (FC1) as one chained
-// persistent launch where it qualifies (gemm_chain_launch), else the two launches.
-int dense_pair(const evt_model* m, const DenseW& wa, const DenseCall& ca, const DenseW& wb,
-               const DenseCall& cb, hipStream_t s) {
-  if (!m->prof && m->chain.sync && (m->fusion & EVT_FUSE_GEMM_CHAIN)) {
-    const GemmParams pa = dense_params(m, wa, ca), pb = dense_params(m, wb, cb);
-    const hipError_t e = gemm_chain_launch(m->dtype, ca.flags, pa, cb.flags, pb, m->chain, s);
-    if (e == hipSuccess) return EVT_OK;
-    if (e != hipErrorNotSupported) EVT_HIP(e, "chained dense");
-  }
-  EVT_RC(dense(m, wa, ca, s));
-  return dense(m, wb, cb, s);
-}
-
-
 // Encoder weights (11 tensors per layer, 12 with the STANDARD qkv bias; evt_vit_num_weights
 // order) for m->heads / m->ffn.
 int build_encoder(evt_model* m, const float* const* w, hipStream_t s) {
@@ -489,30 +470,6 @@ int build_encoder(evt_model* m, const float* const* w, hipStream_t s) {
   return EVT_OK;
 }
 
-// The handle's host-mapped status word (written by kernels with system scope, read by the host
-// after the stream has synchronised: evt_model_status).
-int alloc_status(evt_model* m) {
-  if (m->status) return EVT_OK;
-  void* h = nullptr;
-  EVT_HIP(hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc status");
-  m->status = (unsigned*)h;
-  *m->status = 0;
-  void* d = nullptr;
-  EVT_HIP(hipHostGetDevicePointer(&d, h, 0), "hipHostGetDevicePointer status");
-  m->chain.err = (unsigned*)d;
-  return EVT_OK;
-}
-
-// A failure recorded by an earlier (completed) forward of the handle: EVT_EHIP once, then clear.
-int take_status(evt_model* m) {
-  if (m && m->status && __atomic_load_n(m->status, __ATOMIC_ACQUIRE) != 0) {
-    __atomic_store_n(m->status, 0u, __ATOMIC_RELEASE);
-    return fail(EVT_EHIP, "a chained GEMM hand-off wait timed out in an earlier forward of this "
-                          "handle: its logits are invalid");
-  }
-  return EVT_OK;
-}
-
 // Token-stream workspace of the encoder for B images (hbuf_bytes: the FFN hidden buffer), and the
 // stream-K scratch of the model's GEMMs (its flag block zeroed once; kernels leave it zeroed).
 int alloc_encoder_ws(evt_model* m, int B, size_t hbuf_bytes, hipStream_t s) {
@@ -539,10 +496,6 @@ int alloc_encoder_ws(evt_model* m, int B, size_t hbuf_bytes, hipStream_t s) {
   EVT_HIP(hipMemsetAsync(m->o, 0, ob, s), "memset o");
   EVT_RC(dev_alloc(m, &m->hbuf, hbuf_bytes));
   m->hbuf_bytes = hbuf_bytes;
-  m->chain.sync_bytes = ((rows + 255) / 256 + 3) * 4 + 16;
-  EVT_RC(dev_alloc(m, (void**)&m->chain.sync, m->chain.sync_bytes));
-  EVT_HIP(hipMemsetAsync(m->chain.sync, 0, m->chain.sync_bytes, s), "memset chain words");
-  EVT_RC(alloc_status(m));
   return EVT_OK;
 }
 
@@ -565,37 +518,20 @@ int dense_head(const evt_model* m, const DenseW& w, const DenseCall& c, hipStrea
 }
 
 // Encoder layers (transformer_encoder.py:13-18 / :26-34) on the token stream m->x (+ stats sx).
-// Out-proj -> FC1 run as one chained launch where it qualifies (dense_pair; EVT_FUSE_GEMM_CHAIN,
-// opt-in).
 int run_encoder(evt_model* m, int B, hipStream_t s) {
   const int D = m->D, T = m->sh.T, rows = B * T;
   const float log2e = 1.4426950408889634f;
-  const bool fuse_on = m->dtype == DT_BF16 && D % 64 == 0 && qkv_attn_supported(T, D) &&
-                       (m->fusion & EVT_FUSE_QKV_ATTENTION) != 0;
   for (const Layer& L : m->layers) {
-    const bool fuse = fuse_on && L.hd == 64;
     const float scale_log2 = log2e / std::sqrt((float)L.hd);  // h_k^-0.5 (attention.py:13)
-    if (fuse) {  // LN1-folded QKV + attention in one kernel (qkv_attn.hip)
-      ProfScope ps(m, EVT_PROF_QKV_ATTENTION, s);
-      prof_work(m, 2.0 * rows * D * 3 * L.inner + 4.0 * B * L.heads * (double)T * T * 64,
-                (double)rows * (D + L.inner) * elem_size(m->dtype) +
-                    (double)D * 3 * L.inner * elem_size(m->dtype) + rows * stats_slots(D) * 8.0);
-      QkvAttnParams p{};
-      p.x = m->x; p.ldx = D; p.stats = m->sx; p.nslots = stats_slots(D);
-      p.inv_d = 1.0f / (float)D; p.eps = m->eps;
-      p.W = L.qkv.w; p.ldw = L.qkv.kpad; p.colsum = L.qkv.colsum; p.cvec = L.qkv.b; p.K = L.qkv.kpad;
-      p.inner = L.inner; p.H = L.heads; p.N = T; p.B = B;
-      p.out = m->o; p.ldo = L.inner; p.scale_log2 = 0.125f * log2e;
-      EVT_HIP(qkv_attn_launch(p, s), "qkv_attention");
-    } else {
-      {  // LN1-folded QKV (attention.py:24)
-        ProfScope ps(m, EVT_PROF_QKV, s);
-        DenseCall c;
-        c.flags = EPI_LNIN | EPI_BIAS;
-        c.A = m->x; c.lda = D; c.C = m->qkv; c.ldc = 3 * L.inner; c.M = rows; c.N = 3 * L.inner;
-        c.stats_in = m->sx;
-        EVT_RC(dense(m, L.qkv, c, s));
-      }
+    {  // LN1-folded QKV (attention.py:24)
+      ProfScope ps(m, EVT_PROF_QKV, s);
+      DenseCall c;
+      c.flags = EPI_LNIN | EPI_BIAS;
+      c.A = m->x; c.lda = D; c.C = m->qkv; c.ldc = 3 * L.inner; c.M = rows; c.N = 3 * L.inner;
+      c.stats_in = m->sx;
+      EVT_RC(dense(m, L.qkv, c, s));
+    }
+    {
       ProfScope ps(m, EVT_PROF_ATTENTION, s);
       prof_work(m, 4.0 * B * L.heads * (double)T * T * L.hd,
                 (double)rows * 4 * L.inner * elem_size(m->dtype));  // qkv read + O written
@@ -615,13 +551,11 @@ int run_encoder(evt_model* m, int B, hipStream_t s) {
     c1.flags = EPI_LNIN | EPI_BIAS | (m->standard ? EPI_GELU_ERF : EPI_GELU);
     c1.A = m->xm; c1.lda = D; c1.C = m->hbuf; c1.ldc = L.ffn_st; c1.M = rows; c1.N = L.ffn_st;
     c1.stats_in = m->sm;
-    if (!m->prof) {  // chained where it qualifies (one role per bracketed launch when profiling)
-      EVT_RC(dense_pair(m, L.out, co, L.fc1, c1, s));
-    } else {
-      {
-        ProfScope ps(m, EVT_PROF_OUT_PROJ, s);
-        EVT_RC(dense(m, L.out, co, s));
-      }
+    {
+      ProfScope ps(m, EVT_PROF_OUT_PROJ, s);
+      EVT_RC(dense(m, L.out, co, s));
+    }
+    {
       ProfScope ps(m, EVT_PROF_FC1, s);
       EVT_RC(dense(m, L.fc1, c1, s));
     }
@@ -863,7 +797,6 @@ int evt_model_destroy(evt_model* m) {
   if (m->graph) (void)hipGraphDestroy(m->graph);
   for (hipEvent_t e : m->prof_ev) (void)hipEventDestroy(e);
   for (void* p : m->allocs) (void)hipFree(p);
-  if (m->status) (void)hipHostFree(m->status);
   delete m;
   return EVT_OK;
 }
@@ -958,7 +891,6 @@ int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* 
   if (m->family != 0) return fail(EVT_EINVAL, "model is not a ViT (use evt_t2t_forward)");
   if (B <= 0 || B > m->max_batch)
     return fail(EVT_EINVAL, "batch must be in [1, max_batch=" + std::to_string(m->max_batch) + "]");
-  EVT_RC(take_status(m));
   hipStream_t s = (hipStream_t)stream;
   const evt_vit_desc& d = m->desc;
   const Shape& sh = m->sh;
@@ -1319,14 +1251,8 @@ int evt_graph_capture(evt_model* m, const float* img, int batch, float* logits, 
 
 int evt_graph_launch(evt_model* m, void* stream) {
   if (!m || !m->graph_exec) return fail(EVT_EINVAL, "no captured graph (call evt_graph_capture)");
-  EVT_RC(take_status(m));
   EVT_HIP(hipGraphLaunch(m->graph_exec, (hipStream_t)stream), "graph launch");
   return EVT_OK;
-}
-
-int evt_model_status(evt_model* m) {
-  if (!m) return fail(EVT_EINVAL, "model is NULL");
-  return take_status(m);
 }
 
 // ---- Swin Transformer -------------------------------------------------------------------
@@ -1632,31 +1558,9 @@ int evt_patch_merge(int dtype, const void* x, int64_t ldx, int B, int R, int C, 
 
 // ---- op-level entry points --------------------------------------------------------------
 
-int evt_model_set_fusion(evt_model* m, int flags) {
-  if (!m) return fail(EVT_EINVAL, "model is NULL");
-  if (flags & ~(EVT_FUSE_QKV_ATTENTION | EVT_FUSE_GEMM_CHAIN))
-    return fail(EVT_EINVAL, "unknown fusion flag");
-  m->fusion = flags;
-  return EVT_OK;
-}
-
-int evt_model_set_chain_spin(evt_model* m, int64_t polls) {
-  if (!m) return fail(EVT_EINVAL, "model is NULL");
-  if (polls > 0xffffffffll) return fail(EVT_EINVAL, "polls must be <= 2^32 - 1");
-  m->chain.spin = polls < 0 ? ChainWords{}.spin : (unsigned)polls;
-  return EVT_OK;
-}
-
-int evt_diag_occupy(int blocks, int usec, void* stream) {
-  if (blocks <= 0 || usec < 0 || usec > 10000000)
-    return fail(EVT_EINVAL, "blocks must be positive and usec in [0, 1e7]");
-  EVT_HIP(occupy_launch(blocks, usec, (hipStream_t)stream), "occupy");
-  return EVT_OK;
-}
-
 int evt_set_gemm_variant(int variant) {
   if (!gemm_variant_supported(variant))
-    return fail(EVT_EINVAL, "variant must be 0, 1, 2, 6, 8, 9, 16, 30, 31, 32, 34 or 35 (lab builds: also "
+    return fail(EVT_EINVAL, "variant must be 0, 1, 2, 6, 8, 9, 16, 30 or 31 (lab builds: also "
                             "10, 11, 13, 15, 17-25, 106, 108)");
   gemm_set_variant(variant);
   return EVT_OK;
@@ -1850,22 +1754,6 @@ int evt_attention(int dtype, const void* qkv, int64_t ldq, void* out, int64_t ld
     return fail(EVT_EINVAL, "attention: bad shape (N <= 256, head size 64, 16-B aligned rows)");
   AttnParams p{qkv, ldq, out, ldo, N, H, B, scale * 1.4426950408889634f};
   EVT_HIP(attention_launch(dtype, p, (hipStream_t)stream), "attention");
-  return EVT_OK;
-}
-
-int evt_qkv_attention(const void* x, int D, const float* stats, const void* Wp, const float* colsum,
-                      const float* cvec, int B, int N, int H, float scale, float eps, void* out,
-                      int64_t ldo, void* stream) {
-  if (!x || !stats || !Wp || !colsum || !cvec || !out || B < 0 || H <= 0 || D <= 0 || D % 64 ||
-      !qkv_attn_supported(N, D) || ldo < H * 64)
-    return fail(EVT_EINVAL, "qkv_attention: bad shape (192 < N <= 208, D % 64 == 0, head size 64)");
-  QkvAttnParams p{};
-  p.x = x; p.ldx = D; p.stats = stats; p.nslots = stats_slots(D);
-  p.inv_d = 1.0f / (float)D; p.eps = eps;
-  p.W = Wp; p.ldw = D; p.colsum = colsum; p.cvec = cvec; p.K = D;
-  p.inner = H * 64; p.H = H; p.N = N; p.B = B;
-  p.out = out; p.ldo = ldo; p.scale_log2 = scale * 1.4426950408889634f;
-  EVT_HIP(qkv_attn_launch(p, (hipStream_t)stream), "qkv_attention");
   return EVT_OK;
 }
 

@@ -66,22 +66,6 @@ constexpr int PAD_K = 64;   // K granularity (elements) of every packed operand
 constexpr int PAD_N = 64;   // column granularity of activation buffers
 
 hipError_t gemm_launch(int dtype, int flags, const GemmParams& p, hipStream_t s);
-// Hand-off words of chained launches: sync (>= panels + 3 words, zero when allocated; every
-// launch leaves them zeroed), err (device view of a host-mapped status word: set to 1 when a
-// bounded hand-off wait gives up), spin (poll bound of one wait, ~0.1 us per poll).
-struct ChainWords {
-  unsigned* sync = nullptr;
-  size_t sync_bytes = 0;
-  unsigned* err = nullptr;
-  unsigned spin = 1u << 23;
-};
-// Producer (fa: out-proj with the LN residual and row statistics) and consumer (fb: the LN-
-// folded FC1 + GELU reading the producer's output) in one persistent launch, tiles dequeued in
-// walk order, per-panel hand-offs. hipErrorNotSupported: launch them separately.
-hipError_t gemm_chain_launch(int dtype, int fa, const GemmParams& pa, int fb, const GemmParams& pb,
-                             const ChainWords& cw, hipStream_t s);
-// Diagnostics: `blocks` workgroups holding one CU each (all of its LDS) for `usec` microseconds.
-hipError_t occupy_launch(int blocks, int usec, hipStream_t s);
 // Skinny GEMM (small M, long K: the classifier head) as S K-splits in one launch, fp32 partials
 // part[S][M][ntiles*128], then a fixed-order reduction + bias (+ GELU) into C (deterministic).
 // flags: EPI_BIAS and/or EPI_GELU and/or EPI_OUT_F32 only; K % (S * 64) == 0.
@@ -92,7 +76,7 @@ void gemm_set_variant(int v);
 // Bytes of the stream-K scratch of one GEMM stream (flags block first, zero it once after
 // allocating: the kernel leaves every flag at 0); gemm_sk_bind splits it into the two arrays.
 size_t gemm_sk_bytes();
-void gemm_sk_bind(void* ws, GemmParams& p);  // 0 auto, 1 force 128x128 tiles, 2 force 256x256 (bf16)
+void gemm_sk_bind(void* ws, GemmParams& p);
 hipError_t pack_weight(int dtype, const float* W, const float* row_scale, int K, int N, void* Wp,
                        int Kpad, int Npad, hipStream_t s);
 hipError_t to_bf16_launch(const float* x, void* y, int64_t n, hipStream_t s);  // y[i] = bf16(x[i])
@@ -118,25 +102,7 @@ struct AttnParams {
 };
 hipError_t attention_launch(int dtype, const AttnParams& p, hipStream_t s);
 
-// Fused LN1-folded QKV projection + attention (qkv_attn.hip, bf16): x rows [B*N][ldx] raw token
-// stream, stats [B*N][nslots][2] its slab statistics, W the packed LN-folded Wqkv (rows (qkv h d),
-// ldw = K = Kpad), colsum / cvec per packed row; O rows [B*N][ldo], columns (h d).
-struct QkvAttnParams {
-  const void* x; int64_t ldx;
-  const float* stats; int nslots;
-  float inv_d, eps;
-  const void* W; int64_t ldw;
-  const float* colsum; const float* cvec;
-  int K;          // Kpad: multiple of 64 (the x rows are read up to K: ldx >= K, zero padded)
-  int inner;      // H * 64
-  int H, N, B;
-  void* out; int64_t ldo;
-  float scale_log2;
-  int dbg;        // lab-build ablations (-DEVT_QA_DBG=n): 1 no attention, 2 main loop only,
-                  // 3 one workgroup per CU
-};
-bool qkv_attn_supported(int N, int K);
-hipError_t qkv_attn_launch(const QkvAttnParams& p, hipStream_t s);
+
 
 // LayerNorm over rows of D (fp32 in) -> activation dtype out (eps 1e-5).
 hipError_t layernorm_launch(int dtype, const float* x, int64_t ldx, void* y, int64_t ldy,
@@ -272,8 +238,7 @@ int gemm_variant();  // the calling thread's evt_set_gemm_variant value (0 = aut
 // automatic kernel selection (0; 30 / 31 only steer the 128 x 384 tiles): fused kernels allowed
 inline bool gemm_auto() {
   const int v = gemm_variant();
-  return v == 0 || v == 30 || v == 31 || v == 32 || v == 33 || v == 34 ||
-         v == 35;  // (33: EVT_RIA lab builds; 34 / 35: XCD groups of the persistent walk)
+  return v == 0 || v == 30 || v == 31;
 }
 bool gemm_variant_supported(int v);  // compiled into this build (lab variants: EVT_GEMM_LAB)
 

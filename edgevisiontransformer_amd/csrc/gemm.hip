@@ -494,24 +494,20 @@ constexpr int BIG_STAGE = 2 * BIG_TILE;       // 64 KiB per K-tile
 
 // evt_set_gemm_variant, per calling thread (launch decisions are made on the launching thread):
 // 0 auto, 1 force 128x128, 2 / 6 / 8 non-persistent 256x256 main loops, 9 tile-persistent,
-// 16 stream-K, 30 128 x 384 persistent wherever it applies, 31 automatic without it, 32 automatic
-// with the round-3 tile rule (256x256 only from 256 tiles up). Lab builds (-DEVT_GEMM_LAB) add the ablation / timeline / A-B variants 10, 11, 13,
-// 15, 17-25, 106, 108 used by scripts/gemm_bench.py and scripts/probe/pers_timeline.py.
+// 16 stream-K, 30 128 x 384 persistent wherever it applies, 31 automatic without it. Lab builds
+// (-DEVT_GEMM_LAB) add the ablation / timeline / A-B variants 10, 11, 13, 15, 17-25, 106, 108 used
+// by scripts/gemm_bench.py and scripts/probe/pers_timeline.py. (Round-4 main-loop experiments
+// measured slower - B-fragment prefetch, buffer-descriptor loader, residual in the main loop,
+// residual L2 prefetch, phase-level lgkmcnt waits, DMA-first phases, MFMA priority - were removed
+// in round 5; DESIGN.md records them and git history holds the code.)
 thread_local int g_gemm_variant = 0;
-// Lab A/B: -DEVT_EPI_PACK_FIRST=0 (persistent epilogue without residual: swap fp32 rows, then pack)
-#ifndef EVT_EPI_PACK_FIRST
-#define EVT_EPI_PACK_FIRST 1
-#endif
 
 int num_cus();
 
 bool use_big(const GemmParams& p, int flags) {
   if ((p.ntiles * GEMM_BN) % BIG_BN) return false;
   if (!(flags & EPI_OUT_F32) && p.vec_ok < 2) return false;  // big epilogue: 16-B bf16 stores only
-  // 31: automatic without 128 x 384; 32: automatic with the round-3 rule (>= 256 big tiles)
-  const int v = (g_gemm_variant == 31 || g_gemm_variant == 32 || g_gemm_variant == 33 ||
-                 g_gemm_variant == 34 || g_gemm_variant == 35)
-                    ? 0 : g_gemm_variant;  // (33: EVT_RIA lab builds; 34 / 35: XCD groups)
+  const int v = g_gemm_variant == 31 ? 0 : g_gemm_variant;  // 31: automatic without 128 x 384
   if (v == 1) return false;
   if (v >= 2) return true;
   // 256x256 tiles unless their rounds cost more: time in 256-tile units, the 128x128 kernel at a
@@ -521,7 +517,6 @@ bool use_big(const GemmParams& p, int flags) {
   const int64_t G = num_cus();
   const int64_t t256 = (int64_t)((p.M + 255) / 256) * (p.ntiles * GEMM_BN / 256);
   const int64_t t128 = (int64_t)((p.M + 127) / 128) * p.ntiles;
-  if (g_gemm_variant == 32) return t256 >= 256;
   return (t256 + G - 1) / G <= 0.5 * (double)((t128 + G - 1) / G);
 }
 
@@ -575,46 +570,6 @@ __device__ __forceinline__ void big_epilogue(const GemmParams& p, char* smem, f3
 struct NoOp {
   __device__ void operator()() const {}
 };
-
-// MFMA blocks of the 8-phase loop at raised wave priority (1) or not (0, the product setting:
-// measured round 3 in alternating same-box runs, lab build EVT_LAB_DEFS=-DEVT_MFMA_PRIO=...:
-// without s_setprio DeiT-base +0.4 % in 5 of 5 pairs, T2T-ViT-14 +0.55 %, Swin-T +0.37 %)
-#ifndef EVT_MFMA_PRIO
-#define EVT_MFMA_PRIO 0
-#endif
-// every fragment read of a phase waited for before its first MFMA (1), or the compiler's
-// per-operand lgkmcnt waits (0, the product setting: the first MFMAs start as their own
-// fragments land; +0.4 % DeiT-base in 3 of 3 alternating same-box pairs, round 3)
-#ifndef EVT_PHASE_LGKM0
-#define EVT_PHASE_LGKM0 0
-#endif
-// each phase issues its DMA before (1) or after (0) its fragment reads (lab A/B)
-#ifndef EVT_DMA_FIRST
-#define EVT_DMA_FIRST 0
-#endif
-// the persistent epilogue's per-wave LDS transpose waits for its writes / reads to complete
-// (lgkmcnt(0), 1) or relies on the in-order execution of one wave's LDS operations (0, the
-// product setting: +0.26 % DeiT-base in 3 of 3 alternating pairs; the repeat-launch and model
-// tests bitwise / against fp32 with it, round 3)
-#ifndef EVT_EPI_LGKM0
-#define EVT_EPI_LGKM0 0
-#endif
-// residual GEMMs (out-proj / FC2): L2 prefetch of the epilogue's residual tile at the start of
-// phase 3 of K-tile nk - 1 - EVT_RES_PF (0: none)
-#ifndef EVT_RES_PF
-#define EVT_RES_PF 0
-#endif
-// 256 x 256 geometry: phase 3 of each K-tile but the last reads the NEXT K-tile's W n-half-0
-// fragments into the registers B n-half 1 leaves free (1), so that phase 0 reads 8 fragments
-// instead of 12 (the ping-pong partner's MFMA block covers 4 / 8 / 8 / 4 reads per phase instead
-// of 12 / 4 / 8 / 0); the regions of a K-tile are then DMA'd W n-half 0 first (j = 0 <-> 1), so
-// that region keeps four phases of flight time before the phase-2 wait that retires it. 0: the
-// product schedule (measured round 4, lab EVT_LAB_DEFS=-DEVT_BPF=1 against it in 3 alternating
-// same-box pairs: DeiT-base 28.35k vs 28.64k img/s, QKV / FC1 unchanged, out-proj / FC2 +6 / +9 us
-// from the spills it causes: phase 0's fragment reads do not bound the loop)
-#ifndef EVT_BPF
-#define EVT_BPF 0
-#endif
 
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -689,27 +644,6 @@ __device__ __forceinline__ const char* gather_addr(const GemmParams& p, int gm, 
   return (const char*)p.A + (src * p.lda + c) * 2;
 }
 
-// 256 x 256 plain loaders (lab A/B): the DMA pieces as buffer_load ... lds through a per-tile
-// descriptor (SGPR base at the panel's first row, rows past M read zeros) with one tile-invariant
-// 32-bit lane offset per operand and the K-tile / row-group offset in soffset (1), instead of
-// global_load_lds on a 64-bit address formed per piece (0, the product: ~8 VALU per piece).
-// Measured round 4: 16-24 fewer VGPRs in every persistent kernel and no spills, yet DeiT-base
-// 27.7k vs 28.9k img/s in 3 of 3 alternating same-box runs (scripts/gpu_r4_ria.sh): not kept
-#ifndef EVT_BDMA
-#define EVT_BDMA 0
-#endif
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t dma_rsrc(const void* mat, int64_t ld, int rows,
-                                                          int r0) {
-  r0 = __builtin_amdgcn_readfirstlane(r0);
-  rows = __builtin_amdgcn_readfirstlane(rows);
-  return __builtin_amdgcn_make_buffer_rsrc((char*)const_cast<void*>(mat) + (int64_t)r0 * ld * 2, 0,
-                                           max(0, min(rows - r0, 256)) * (int)ld * 2, 0x00020000);
-}
-__device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, int voff, int soff,
-                                       EVT_LDS void* lds_base) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, lds_base, 16, voff, soff, 0, 0);
-}
-
 // DMA region j of K-tile T into buffer (T ^ par) & 1 (par: the buffer parity of the tile's
 // K-tile 0; persistent kernel with an odd K-tile count: alternates from tile to tile).
 template <typename P>
@@ -746,7 +680,6 @@ __device__ __forceinline__ void big8_stage(const P& p, char* smem, int wave, int
     ins(2 * j + 1);
     return;
   }
-  if (EVT_BPF) j = j < 2 ? 1 - j : j;  // DMA order W n-half 0, A m-half 0, W n-half 1, A m-half 1
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int r = (wave * 2 + i) * 8;  // region row of this wave-instruction (8 rows)
@@ -757,25 +690,12 @@ __device__ __forceinline__ void big8_stage(const P& p, char* smem, int wave, int
         glds16(gather_addr<1>(p, gm, T * 64 + ((sslot ^ srow) << 3)), base + row * ROWB);
       else if constexpr (std::is_same<P, UnfoldParams>::value)
         glds16(gather_addr<2>(p, gm, T * 64 + ((sslot ^ srow) << 3)), base + row * ROWB);
-      else if (EVT_BDMA)  // one lane offset per wave (instruction i, region j: + 8 i, + 64 rows)
-        bdma16(dma_rsrc(p.A, p.lda, p.M, m0),
-               (((wave * 16) & 63) + (((wave * 16) >> 6) << 7) + srow) * ((int)p.lda * 2) +
-                   ((sslot ^ srow) << 4),
-               __builtin_amdgcn_readfirstlane(T * ROWB + (8 * i + (j == 3 ? 64 : 0)) * (int)p.lda * 2),
-               base + row * ROWB);
       else
         glds16((const char*)p.A + (int64_t)gm * (p.lda * 2) + koff, base + row * ROWB);
     } else {
       const int row = ((r >> 5) << 6) + (r & 31) + (j == 2 ? 32 : 0);
-      if (EVT_BDMA)  // (the packed weight has its rows padded to the 256-wide tiles)
-        bdma16(dma_rsrc(p.W, p.ldw, n0 + 256, n0),
-               ((((wave * 16) >> 5) << 6) + ((wave * 16) & 31) + srow) * ((int)p.ldw * 2) +
-                   ((sslot ^ srow) << 4),
-               __builtin_amdgcn_readfirstlane(T * ROWB + (8 * i + (j == 2 ? 32 : 0)) * (int)p.ldw * 2),
-               base + BIG_TILE + row * ROWB);
-      else
-        glds16((const char*)p.W + (int64_t)(n0 + row + srow) * (p.ldw * 2) + koff,
-               base + BIG_TILE + row * ROWB);
+      glds16((const char*)p.W + (int64_t)(n0 + row + srow) * (p.ldw * 2) + koff,
+             base + BIG_TILE + row * ROWB);
     }
   }
 }
@@ -804,62 +724,15 @@ __device__ __forceinline__ void big8_prologue(const P& p, char* smem, int wave, 
 // final MFMA phase and group 0 the resync barrier after the loop, so group 0 starts its epilogue
 // while group 1 still issues its last 16 MFMAs (the two barriers cancel in every wave's count).
 // ph3: issues X3 further VMEM loads at the start of phase 3 (added to that phase's wait).
-// CARRY (EVT_BPF, 256 x 256): bit 0, B n-half-0 fragments come in *bc (read by the previous
-// K-tile's phase 3); bit 1, phase 3 reads the next K-tile's into *bc (its region retired by a
-// phase-2 wait).
-// RT (PERS_RIA: a persistent residual GEMM whose residual is added into the accumulators by the
-// main loop instead of fetched by the epilogue; nk >= RIA_NK): K-tiles 1 .. 9 run unrolled as
-// RT = t. The odd K-tiles 1, 3, 5, 7 load the residual of one 16-column group nt = (t - 1) / 2 of
-// the wave's 128 x 64 block (8-B loads in the accumulator layout, mt 2 ph and 2 ph + 1 in phase
-// ph, right after the phase's wait, into slots mt); K-tile t + 2 adds them (mt 0-3 in phase 0,
-// 4-5 in 1, 6-7 in 2, each before that accumulator's MFMA of the K-tile) after its phase-0 wait
-// has retired the DMA issued after the last of them. Every element of column group nt thus gets
-// its residual after exactly (2 nt + 3) K-tile contributions, whatever its row: the rounding does
-// not depend on a row's position in the tile (batch-position independence). The residual's HBM
-// stream is spread over the loop instead of a 128 KB burst per tile in the epilogue. The loads
-// count in vmcnt (issue order): an odd K-tile's wait keeps its earlier phases' 2 ph loads in
-// flight besides the 8 younger DMAs, an even K-tile's the 2 (4 - ph) loads of the previous one.
-constexpr int RIA_NK = 12;
-// (lab A/B, EVT_LAB_DEFS=-DEVT_RIA=1: measured round 4 with the buffer-descriptor loader, where
-// it fits in registers: DeiT-base 26.5k vs 27.7k img/s without it in 3 of 3 alternating runs; with
-// the global_load_lds loader it spills in the loop. Not kept: the product fetches the residual in
-// the epilogue)
-#ifndef EVT_RIA
-#define EVT_RIA 0
-#endif
-template <int BASE, int A0, int A1, int A3>
-__device__ __forceinline__ void wait_ph(int ph) {  // (no wait in phase 2)
-  if (ph == 0) wait_vm<BASE + A0>();
-  else if (ph == 1) wait_vm<BASE + A1>();
-  else if (ph == 3) wait_vm<BASE + A3>();
-}
-struct NoRh {
-  template <typename A>
-  __device__ void add(A&, int, int) {}
-  __device__ void issue(int, int) {}
-};
-
-template <int NH>
-struct BCarry {
-  u32x4 v[NH][2];
-};
-template <int MODE, int X, int CARRY = 0, int RT = 0, bool OPEN = false, int X3 = 0,
-          typename Ph3 = NoOp, typename P = GemmParams, typename Rh = NoRh>
+template <int MODE, int X, bool OPEN = false, int X3 = 0, typename Ph3 = NoOp,
+          typename P = GemmParams>
 __device__ __forceinline__ void big8_ktile(const P& p, char* smem,
                                            f32x4 (&acc)[GeoOf<P>::NF][GeoOf<P>::MF],
                                            int wave, int lane, int wm, int wn, int m0, int n0,
                                            int t, bool cont = false, int nm0 = 0, int nn0 = 0,
-                                           Ph3 ph3 = {}, int par = 0, int npar = 0,
-                                           bool x3on = true, BCarry<Geo<P>::NH>* bc = nullptr,
-                                           Rh* rh = nullptr) {
+                                           Ph3 ph3 = {}, int par = 0, int npar = 0) {
   typedef Geo<P> Gm;
   constexpr int MH = Gm::MH, NH = Gm::NH;
-  constexpr bool HAS = CARRY & 1, PFN = CARRY & 2;
-  static_assert(CARRY == 0 || (Gm::BM == 256 && EVT_BPF), "carry: 256 x 256 DMA order only");
-  static_assert(!PFN || MODE < 2, "the last K-tile has no next K-tile");
-  static_assert(RT == 0 || (X3 == 0 && Gm::BM == 256 && MODE == 0 && X == 0 && RT <= 9),
-                "residual chunks: 256 x 256 steady K-tiles 1 .. 9");
-  constexpr bool RLOAD = (RT & 1) && RT <= 7, RADD = (RT & 1) && RT >= 3;
   const int frow = lane & 15, fsw = lane & 7, fg = lane >> 4;
   const EVT_LDS char* As = (const EVT_LDS char*)smem + ((t ^ par) & 1) * BIG_STAGE;
   const EVT_LDS char* Ws = As + Gm::A_TILE;
@@ -869,90 +742,45 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem,
   u32x4 af[MH][2], bf0[NH][2], bf1[NH][2];
 #pragma unroll
   for (int ph = 0; ph < 4; ++ph) {
-    auto reads = [&]() {
-      if (ph == 0) {
+    // the phase's fragment reads, then its DMA issue (the DMA regions are >= 2 phases from any
+    // read here; issuing the DMA first measured 0.7 % slower, round 3)
+    if (ph == 0) {
 #pragma unroll
-        for (int nt = 0; nt < NH; ++nt)
+      for (int nt = 0; nt < NH; ++nt)
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks)
-            bf0[nt][ks] = HAS ? bc->v[nt][ks] : rd(Ws, wn * Gm::WC + nt * 16 + frow, ks);
+        for (int ks = 0; ks < 2; ++ks) bf0[nt][ks] = rd(Ws, wn * Gm::WC + nt * 16 + frow, ks);
 #pragma unroll
-        for (int mt = 0; mt < MH; ++mt)
+      for (int mt = 0; mt < MH; ++mt)
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) af[mt][ks] = rd(As, wm * Gm::WR + mt * 16 + frow, ks);
-      } else if (ph == 1) {
+        for (int ks = 0; ks < 2; ++ks) af[mt][ks] = rd(As, wm * Gm::WR + mt * 16 + frow, ks);
+    } else if (ph == 1) {
 #pragma unroll
-        for (int nt = 0; nt < NH; ++nt)
+      for (int nt = 0; nt < NH; ++nt)
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks)
-            bf1[nt][ks] = rd(Ws, wn * Gm::WC + Gm::WC / 2 + nt * 16 + frow, ks);
-      } else if (ph == 2) {
+        for (int ks = 0; ks < 2; ++ks)
+          bf1[nt][ks] = rd(Ws, wn * Gm::WC + Gm::WC / 2 + nt * 16 + frow, ks);
+    } else if (ph == 2) {
 #pragma unroll
-        for (int mt = 0; mt < MH; ++mt)
+      for (int mt = 0; mt < MH; ++mt)
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks)
-            af[mt][ks] = rd(As, wm * Gm::WR + Gm::WR / 2 + mt * 16 + frow, ks);
-      } else if (PFN) {  // ph 3: the next K-tile's B n-half 0 (its buffer, region j = 0)
-        const EVT_LDS char* Wn =
-            (const EVT_LDS char*)smem + (((t + 1) ^ par) & 1) * BIG_STAGE + Gm::A_TILE;
-#pragma unroll
-        for (int nt = 0; nt < NH; ++nt)
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) bc->v[nt][ks] = rd(Wn, wn * Gm::WC + nt * 16 + frow, ks);
-      }
-    };
-    auto dmas = [&]() {
-      if (ph == 3) ph3();
-      // DMA of region s = 4 t + ph + 6
-      if (MODE == 0 || (MODE == 1 && ph < 2)) {
-        if (ph < 2) big8_stage(p, smem, wave, lane, m0, n0, t + 1, ph + 2, par);
-        else big8_stage(p, smem, wave, lane, m0, n0, t + 2, ph - 2, par);
-      } else if (cont) {  // MODE 1 phases 2, 3 and MODE 2: the next tile's regions, in order
-        const int s6 = (MODE == 1 ? ph - 2 : ph + 2);  // 0..5: (K-tile 0, regions 0-3), (1, 0-1)
-        big8_stage(p, smem, wave, lane, nm0, nn0, s6 >> 2, s6 & 3, npar);
-      }
-    };
-    // the phase's fragment reads and its DMA issue (the DMA regions are >= 2 phases from any read
-    // here; the order does not change how many VMEM ops are younger than a region's DMA)
-#if EVT_DMA_FIRST
-    dmas();
-    reads();
-#else
-    reads();
-    dmas();
-#endif
+        for (int ks = 0; ks < 2; ++ks)
+          af[mt][ks] = rd(As, wm * Gm::WR + Gm::WR / 2 + mt * 16 + frow, ks);
+    }
+    if (ph == 3) ph3();
+    // DMA of region s = 4 t + ph + 6
+    if (MODE == 0 || (MODE == 1 && ph < 2)) {
+      if (ph < 2) big8_stage(p, smem, wave, lane, m0, n0, t + 1, ph + 2, par);
+      else big8_stage(p, smem, wave, lane, m0, n0, t + 2, ph - 2, par);
+    } else if (cont) {  // MODE 1 phases 2, 3 and MODE 2: the next tile's regions, in order
+      const int s6 = (MODE == 1 ? ph - 2 : ph + 2);  // 0..5: (K-tile 0, regions 0-3), (1, 0-1)
+      big8_stage(p, smem, wave, lane, nm0, nn0, s6 >> 2, s6 & 3, npar);
+    }
     // retire what the next phase reads (phases 4, 1, 2 precede reading phases). W0: after phase 0
     // the W n-half-1 region must have landed; its last instruction is followed by 8 younger ones
     // in the 256 x 256 order, by 7 in the paired order of the 128 x 384 geometry (big8_stage)
     constexpr int W0 = Gm::WI == 3 ? 7 : 8;
-    if (RT > 0) {  // W0 = 8 in this geometry
-      if (RLOAD) wait_ph<8, 0, 2, 6>(ph);        // this K-tile's loads of phases < ph
-      else if (RT & 1) wait_ph<8, 0, 0, 0>(ph);  // K-tile 9: none since K-tile 7
-      else wait_ph<8, 8, 6, 2>(ph);              // the previous K-tile's loads of phases >= ph
-      if (RADD) {  // column group (RT - 3) / 2, loaded two K-tiles ago
-        constexpr int NT = (RT - 3) / 2;
-        if (ph == 0) {
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt) rh->add(acc[NT][mt], mt, NT);
-        } else if (ph == 1) {
-          rh->add(acc[NT][4], 4, NT);
-          rh->add(acc[NT][5], 5, NT);
-        } else if (ph == 2) {
-          rh->add(acc[NT][6], 6, NT);
-          rh->add(acc[NT][7], 7, NT);
-        }
-      }
-      if (RLOAD) {
-        rh->issue(2 * ph, (RT - 1) / 2);
-        rh->issue(2 * ph + 1, (RT - 1) / 2);
-      }
-    } else if (ph != 2) {
-      if (MODE == 0) {
-        if (ph == 3 && X3 > 0 && x3on) wait_vm<8 + X + X3>();
-        else if (ph == 0) wait_vm<W0 + X>();
-        else wait_vm<8 + X>();
-      }
-      else if (cont) {  // the steady-state DMA pattern continues: steady-state waits
+    if (ph != 2) {
+      if (MODE == 0 || cont) {  // (cont: the steady-state DMA pattern continues)
         if (ph == 3) wait_vm<8 + X + X3>();
         else if (ph == 0) wait_vm<W0 + X>();
         else wait_vm<8 + X>();
@@ -965,20 +793,9 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem,
       } else if (ph == 1) {
         wait_vm<0 + X>();
       }
-    } else if (PFN) {
-      // phase 3 reads the next K-tile's region j = 0, DMA'd 4 phases before this one: 8 younger
-      // instructions in steady state; MODE 1 issues no DMA in this phase unless cont
-      if (MODE == 0 || cont) wait_vm<8 + X>();
-      else wait_vm<6 + X>();
     }
     big8_bar();
-#if EVT_PHASE_LGKM0
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
     __builtin_amdgcn_sched_barrier(0);
-#if EVT_MFMA_PRIO == 1
-    __builtin_amdgcn_s_setprio(1);
-#endif
     const int mb = (ph >= 2) ? MH : 0, nb = (ph == 1 || ph == 2) ? NH : 0;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -987,35 +804,25 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem,
 #pragma unroll
         for (int mt = 0; mt < MH; ++mt)
           Mma<bf16>::run(nb ? bf1[nt][ks] : bf0[nt][ks], af[mt][ks], acc[nb + nt][mb + mt]);
-#if EVT_MFMA_PRIO == 1
-    __builtin_amdgcn_s_setprio(0);
-#endif
     if (!(OPEN && MODE == 2 && ph == 3 && wm == 1)) big8_bar();
   }
 }
 
 // Main loop over the nk K-tiles after big8_prologue (whose DMAs may be followed by X further
 // VMEM instructions per wave, or by a vmcnt(0)). Ends with every wave past a common barrier.
-
 // pre1: run by wave group 1 in the slot where it waits one barrier for group 0 (per-tile LDS
 // setup work that is then off the critical path); mid: after K-tile 0 (nk >= 3 only).
 // last: issues LX further VMEM loads per wave just before the last K-tile (added to its waits:
-// they are younger than every DMA that tile waits for).
-// pf: issues PFX further VMEM loads at the start of phase 3 of steady-state K-tile tpf (added to
-// that phase's wait; the following waits of the next K-tile retire one phase's DMA earlier).
-// rh (PERS_RIA, nk >= RIA_NK): the loop K-tiles carry the residual chunks (big8_ktile RT).
+// they are younger than every DMA that tile waits for); last3: LX3 more at the start of the last
+// K-tile's phase 3.
 template <int X, bool OPEN = false, typename Pre1 = NoOp, typename Mid = NoOp, int LX = 0,
-          typename Last = NoOp, int LX3 = 0, typename Last3 = NoOp, typename P = GemmParams,
-          int PFX = 0, typename Pf = NoOp, typename Rh = NoRh>
+          typename Last = NoOp, int LX3 = 0, typename Last3 = NoOp, typename P = GemmParams>
 __device__ __forceinline__ void big8_loop(const P& p, char* smem,
                                           f32x4 (&acc)[GeoOf<P>::NF][GeoOf<P>::MF],
                                           int wave, int lane, int wm, int wn, int m0, int n0,
                                           int nk, bool cont = false, int nm0 = 0, int nn0 = 0,
                                           Pre1 pre1 = {}, Mid mid = {}, Last last = {},
-                                          Last3 last3 = {}, int par = 0, Pf pf = {}, int tpf = -1,
-                                          Rh* rh = nullptr) {
-  constexpr bool RIA = !std::is_same<Rh, NoRh>::value;
-  static_assert(!RIA || PFX == 0, "residual chunks and the residual L2 prefetch exclude each other");
+                                          Last3 last3 = {}, int par = 0) {
   // K-tile t of this tile sits in buffer (t ^ par) & 1; the next tile (cont) starts at the parity
   // of stream K-tile nk
   const int npar = par ^ (nk & 1);
@@ -1026,57 +833,25 @@ __device__ __forceinline__ void big8_loop(const P& p, char* smem,
     pre1();
     big8_bar();
   }
-  // EVT_BPF carry of B n-half-0 fragments from each K-tile's phase 3 to the next one's phase 0
-  constexpr bool BPF = EVT_BPF && Geo<P>::BM == 256;
-  constexpr int CF = BPF ? 2 : 0, CM = BPF ? 3 : 0, CL = BPF ? 1 : 0;  // first / middle / last
-  BCarry<Geo<P>::NH> bc;
   if (nk >= 3) {
-    big8_ktile<0, X, CF>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, false, 0, 0, {}, par, 0,
-                         true, &bc);
+    big8_ktile<0, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, false, 0, 0, {}, par, 0);
     mid();
     int t = 1;
-    if constexpr (RIA) {  // the launch guarantees nk >= RIA_NK: K-tiles 1 .. 9 are steady
-      auto kt = [&](auto rt) {
-        constexpr int RT = decltype(rt)::value;
-        big8_ktile<0, 0, CM, RT>(p, smem, acc, wave, lane, wm, wn, m0, n0, RT, false, 0, 0, {},
-                                 par, 0, true, &bc, rh);
-      };
-      kt(std::integral_constant<int, 1>{});
-      kt(std::integral_constant<int, 2>{});
-      kt(std::integral_constant<int, 3>{});
-      kt(std::integral_constant<int, 4>{});
-      kt(std::integral_constant<int, 5>{});
-      kt(std::integral_constant<int, 6>{});
-      kt(std::integral_constant<int, 7>{});
-      kt(std::integral_constant<int, 8>{});
-      kt(std::integral_constant<int, 9>{});
-      t = 10;
-    }
-    for (; t + 2 < nk; ++t) {
-      if constexpr (PFX > 0) {
-        const bool on = t == tpf;  // wave-uniform
-        big8_ktile<0, 0, CM, 0, false, PFX>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, false, 0,
-                                         0, [&]() { if (on) pf(); }, par, 0, on, &bc);
-      } else {
-        big8_ktile<0, 0, CM>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, false, 0, 0, {}, par, 0,
-                             true, &bc);
-      }
-    }
-    big8_ktile<1, 0, CM>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, cont, nm0, nn0, {}, par,
-                         npar, true, &bc);
+    for (; t + 2 < nk; ++t)
+      big8_ktile<0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, false, 0, 0, {}, par, 0);
+    big8_ktile<1, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, cont, nm0, nn0, {}, par, npar);
     last();
-    big8_ktile<2, LX, CL, 0, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1, cont, nm0,
-                                     nn0, last3, par, npar, true, &bc);
+    big8_ktile<2, LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1, cont, nm0, nn0,
+                                 last3, par, npar);
   } else if (nk == 2) {
-    big8_ktile<1, X, CF>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, cont, nm0, nn0, {}, par,
-                         npar, true, &bc);
+    big8_ktile<1, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, cont, nm0, nn0, {}, par, npar);
     last();
-    big8_ktile<2, LX, CL, 0, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, 1, cont, nm0, nn0,
-                                     last3, par, npar, true, &bc);
+    big8_ktile<2, LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, 1, cont, nm0, nn0, last3,
+                                 par, npar);
   } else {
     last();
-    big8_ktile<2, X + LX, 0, 0, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, false, 0, 0,
-                                        last3, par);
+    big8_ktile<2, X + LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, false, 0, 0,
+                                     last3, par);
   }
   if (!OPEN && wm == 0) big8_bar();
 }
@@ -1222,12 +997,8 @@ constexpr int PERS_COEF = PERS_COLRAW + 3072;   // LayerNorm (mu, r) per tile ro
 constexpr int PERS_COLB = PERS_COEF + 2048;     // column vectors of the tile being finished
 constexpr int PERS_PART = PERS_COLB + 3072;     // odd-wn waves' row partials [2][256] f32x2
 constexpr int PERS_LDS = PERS_PART + 4096;
-constexpr int PERS_SINK = PERS_LDS + 16;        // 256 B that the residual L2 prefetch DMAs into
-constexpr int PERS_LDS_ALL = PERS_SINK + 256;
+constexpr int PERS_LDS_ALL = PERS_LDS + 16;
 constexpr int PERS_X = 16;                      // output stores per wave per interior tile
-// template-only flag of gemm_pers_kernel (above the EPI_ bits): residual GEMM whose residual is
-// added into the accumulators by the main loop (RiaHook), K >= 64 RIA_NK
-constexpr int PERS_RIA = 1 << 16;
 
 template <int FL>
 struct PersFlags {
@@ -1457,11 +1228,7 @@ __device__ __forceinline__ void pers_epilogue_v1(const GemmParams& p, char* smem
         const int ch = 2 * nt + (fg >> 1);
         *(EVT_LDS u32x4*)(scr + wrow * 128 + ((ch ^ (wrow & 7)) << 4)) = ov[k][nt];
       }
-#if EVT_EPI_LGKM0
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
       asm volatile("" ::: "memory");  // (a wave's LDS operations execute in order)
-#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = i * 8 + rrow;
@@ -1527,51 +1294,6 @@ __device__ __forceinline__ int pos_img(int m, int P) {
 }
 __device__ __forceinline__ int pos_orow(int m, int P) { return m + pos_img(m, P) + 1; }
 
-// PERS_RIA: the tile's residual, chunk (mt, nt) = rows wm 128 + mt 16 + frow, columns
-// wn 64 + nt 16 + 4 fg .. + 3 (the accumulator layout of acc[nt][mt]), 8-B buffer loads through
-// the tile's descriptor (rows past M read 0) into slot mt, added as the epilogue adds it: plain,
-// or the residual LayerNorm gamma (r resid - r mu) (beta stays in the epilogue's bias add).
-template <int FL>
-struct RiaHook {
-  __amdgpu_buffer_rsrc_t rs;
-  int vo, ldr2, rl, cl;
-  const char* smem;
-  u32x2 rv[8];
-  __device__ __forceinline__ RiaHook(const GemmParams& p, const char* sm, int wm, int wn, int lane,
-                                     int m0, int n0) : smem(sm) {
-    const int frow = lane & 15, fg = lane >> 4;
-    rl = wm * 128 + frow;
-    cl = wn * 64 + 4 * fg;
-    ldr2 = (int)p.ldr * 2;
-    rs = tile_rsrc(p.resid, p.ldr, p.M, m0, n0);
-    vo = rl * ldr2 + cl * 2;
-  }
-  __device__ __forceinline__ void issue(int mt, int nt) {
-    const int so = __builtin_amdgcn_readfirstlane(mt * 16 * ldr2 + nt * 32);
-    rv[mt] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, 0));
-  }
-  __device__ __forceinline__ void add(f32x4& a, int mt, int nt) {
-    const bf16x4 r4 = __builtin_bit_cast(bf16x4, rv[mt]);
-    if constexpr ((FL & EPI_RESLN) != 0) {
-      const f32x2 cf = ((const EVT_LDS f32x2*)(smem + PERS_COEF))[rl + mt * 16];
-      const f32x4 g = lds4((const EVT_LDS float*)(smem + PERS_COLB) + 256 + cl + 16 * nt);
-      const f32x2 rr = {cf[1], cf[1]}, nrm = {-cf[1] * cf[0], -cf[1] * cf[0]};
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const f32x2 rv2 = {(float)r4[2 * q], (float)r4[2 * q + 1]};
-        const f32x2 tt = __builtin_elementwise_fma(rr, rv2, nrm);
-        const f32x2 o = __builtin_elementwise_fma(f32x2{g[2 * q], g[2 * q + 1]}, tt,
-                                                  f32x2{a[2 * q], a[2 * q + 1]});
-        a[2 * q] = o[0];
-        a[2 * q + 1] = o[1];
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) a[j] += (float)r4[j];
-    }
-  }
-};
-
 // Epilogue of one 256 x 256 tile straight from the accumulators (VALU-bound: every instruction
 // here is paid with the MFMA pipe idle, so the arithmetic is in packed form throughout):
 //   LNIN   r (acc - mu colsum) + c      2 v_pk_fma per column pair
@@ -1600,16 +1322,7 @@ __device__ __forceinline__ void pers_resid_early(const GemmParams& p, int wm, in
   }
 }
 
-// SC1: chained-launch producer (gemm_chain_kernel): every output byte is stored write-through
-// (sc1: 16-B buffer stores with aux 16, the 8-B row statistics as agent-scope atomic stores) so
-// that a consumer workgroup on another XCD reads it after its agent-scope acquire; otherwise
-// the outputs are non-temporal.
-__device__ __forceinline__ void stats_store_sc1(float* p, f32x2 v) {
-  __hip_atomic_store((unsigned long long*)p, __builtin_bit_cast(unsigned long long, v),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int FL, int DBG = 0, bool PADN = true, int ER = 0, bool SC1 = false>
+template <int FL, int DBG = 0, bool PADN = true, int ER = 0>
 __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f32x4 (&acc)[4][8],
                                               int wave, int wm, int wn, int m0, int n0, int tn,
                                               int lane, bool interior, int iter = 0,
@@ -1620,7 +1333,6 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
       ((unsigned long long*)p.pos)[((int64_t)blockIdx.x * 16 + iter) * 8 + k] = __builtin_amdgcn_s_memtime();
   };
   asm volatile("" : "+v"(lane));  // keep lane-derived addresses out of the persistent loop (VGPRs)
-  constexpr bool RIA = (FL & PERS_RIA) != 0;  // the residual is already in the accumulators
   if constexpr (DBG == 2) {  // ablation: no epilogue at all, accumulators kept live by a dead store
     float sink = 0.f;
 #pragma unroll
@@ -1691,7 +1403,7 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
   //    wn*64 + nt*16 + (fg >> 1)*8 + [acc[nt][2k][0..3], acc[nt][2k+1][0..3]]
   //    (no residual / position / statistics: the values are packed to bf16 first and the swap
   //    moves 2 dwords per pair instead of 4; the same elements, bitwise the same stores)
-  constexpr bool PACK_FIRST = EVT_EPI_PACK_FIRST && (FL & (EPI_RESID | EPI_POS | EPI_STATS)) == 0;
+  constexpr bool PACK_FIRST = (FL & (EPI_RESID | EPI_POS | EPI_STATS)) == 0;
   if constexpr (!PACK_FIRST) {
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
@@ -1711,7 +1423,7 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
     for (int k = 0; k < 4; ++k)
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) rr[k][nt] = u32x4{0u, 0u, 0u, 0u};
-  } else if constexpr ((FL & EPI_RESID) != 0 && !RIA) {
+  } else if constexpr ((FL & EPI_RESID) != 0) {
     const __amdgpu_buffer_rsrc_t rs = tile_rsrc(p.resid, p.ldr, p.M, m0, n0);
     const int vo = (rl * (int)p.ldr + cl) * 2;
 #pragma unroll
@@ -1768,7 +1480,7 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       f32x4 v[2] = {acc[nt][2 * k], acc[nt][2 * k + 1]};
-      if constexpr (((FL & EPI_RESID) != 0 && !RIA) || (FL & EPI_POS) != 0) {
+      if constexpr ((FL & (EPI_RESID | EPI_POS)) != 0) {
         const bf16x8 r8 = __builtin_bit_cast(bf16x8, rr[k][nt]);
         const f32x2 rrow = {rc[k][1], rc[k][1]}, nrm = {-rc[k][1] * rc[k][0], -rc[k][1] * rc[k][0]};
 #pragma unroll
@@ -1835,11 +1547,7 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
         const int ch = 2 * nt + (fg >> 1);
         *(EVT_LDS u32x4*)(scr + wrow * 128 + ((ch ^ (wrow & 7)) << 4)) = ov[k][nt];
       }
-#if EVT_EPI_LGKM0
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
       asm volatile("" ::: "memory");  // (a wave's LDS operations execute in order)
-#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = i * 8 + rrow;
@@ -1854,14 +1562,10 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
           svo = ((pos_orow(m0 + wm * 128 + 32 * k + 8 * i + rrow, p.P) - orow0) * (int)p.ldc +
                  wn * 64 + rch * 8) * 2;
         }
-        if (keep)  // nontemporal (aux nt): whole lines streamed past L2; SC1: write-through
-          buffer_store_b128<SC1 ? 16 : 2>(v, cs, svo, so);
+        if (keep)  // nontemporal (aux nt): whole lines streamed past L2
+          buffer_store_b128<2>(v, cs, svo, so);
       }
-#if EVT_EPI_LGKM0
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
       asm volatile("" ::: "memory");
-#endif
     }
   }
   stamp(5);
@@ -1885,107 +1589,11 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
         const int m = m0 + rl + 32 * k;
         const f32x2 o = part[rl + 32 * k];
         const int sm = (FL & EPI_POS) ? pos_orow(m, p.P) : m;
-        if (interior || m < p.M) {
-          float* so = p.stats_out + 2 * ((int64_t)p.nslots * sm + 2 * tn + (wn >> 1));
-          if constexpr (SC1)
-            stats_store_sc1(so, st[k] + o);
-          else
-            *(f32x2*)so = st[k] + o;
-        }
+        if (interior || m < p.M)
+          *(f32x2*)(p.stats_out + 2 * ((int64_t)p.nslots * sm + 2 * tn + (wn >> 1))) = st[k] + o;
       }
     }
   }
-}
-
-// Chained launches (gemm_chain_kernel): a producer GEMM's tiles, then a consumer GEMM whose M
-// panel p may start once the producer's tiles of panel p are stored. ChainCtx is the block's view
-// of the hand-off words (zeroed by the launch): cnt[p] = producer tiles of panel p published,
-// gdone = producer tiles published in all, head = the next walk index to hand out; err = the
-// handle's host-mapped status word (a bounded wait gave up: evt_model_status reports it).
-//
-// Tiles are DEQUEUED in walk order (producer tiles 0 .. totalA - 1, then the consumer's), not
-// assigned by block index: a tile is only ever waited on after some running block has claimed it,
-// and a block's claims are increasing, so the lowest unfinished tile is always the current tile of
-// a running block whose dependencies (lower walk indices) are all finished. The walk progresses
-// whatever the residency (another stream's kernel may hold CUs, blocks may start late): no
-// co-residency assumption, no cooperative launch. A block holds its current tile, the next one
-// (whose prologue its main loop prefetches) and the ticket it takes at the top of the current tile,
-// read after that tile's epilogue (no wait on the atomic anywhere in the main loop).
-struct ChainCtx {
-  int base = 0;         // walk index of the running stage's tile 0
-  int cur = 0, nxt = 0; // walk indices: the block's current tile and the one after (uniform)
-  unsigned tk = 0;      // thread 0: the ticket taken at the top of the current tile (read after
-                        // the tile's counted waits have retired it)
-  bool all_ready = false;
-};
-// The launch constants of the hand-off live in LDS (read at tile boundaries only): kept out of
-// the registers of the main loop, which has none to spare.
-struct ChainConst {
-  unsigned* cnt;
-  unsigned* gdone;
-  unsigned* head;
-  unsigned* err;
-  unsigned need;    // producer tiles per panel
-  unsigned totalA;  // producer tiles
-  unsigned total;   // producer + consumer tiles (walk length)
-  unsigned spin;    // poll bound of a hand-off wait (iterations of ~0.1 us)
-};
-
-constexpr int CHAIN_WORD = PERS_LDS;        // LDS broadcast word (the kernels allocate PERS_LDS + 16)
-constexpr int CHAIN_TICKET = PERS_LDS + 4;  // the ticket read at the last epilogue
-constexpr int CHAIN_CONST = PERS_LDS_ALL;   // ChainConst (gemm_chain_kernel only)
-constexpr int CHAIN_LDS_ALL = CHAIN_CONST + (int)sizeof(ChainConst);
-
-__device__ __forceinline__ const EVT_LDS ChainConst& chain_const(const char* smem) {
-  return *(const EVT_LDS ChainConst*)(smem + CHAIN_CONST);
-}
-
-// Producer: publish panel tm (one lane, behind a barrier that every storing wave reached after its
-// vmcnt(0) drain: the guide's R1 form with write-through stores).
-__device__ __forceinline__ void chain_publish(const char* smem, int tm) {
-  const EVT_LDS ChainConst& k = chain_const(smem);
-  __hip_atomic_fetch_add(k.cnt + tm, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_fetch_add(k.gdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Thread 0: dequeue the next walk index into cx.tk (while the walk lasts). The atomic is inline asm
-// so that the compiler places no wait for its result: the caller reads cx.tk only after counted
-// vmcnt waits that retire it.
-__device__ __forceinline__ void chain_take_ticket(ChainCtx& cx, const char* smem) {
-  const EVT_LDS ChainConst& k = chain_const(smem);
-  if (cx.tk < k.total) {
-    unsigned* h = k.head;
-    unsigned one = 1u, r;
-    asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(r) : "v"(h), "v"(one) : "memory");
-    cx.tk = r;
-  }
-}
-
-// Consumer: wait (all threads, block-uniform) until panel tm is published, then one agent-scope
-// acquire; once an acquire has followed the observation that every producer tile is published,
-// later tiles need neither. Bounded (cx.spin polls): on timeout the handle's status word is set
-// (the forward is reported failed, never silently wrong) and the block goes on.
-__device__ __forceinline__ void chain_wait(ChainCtx& cx, int tm, char* smem) {
-  if (cx.all_ready) return;
-  if (threadIdx.x == 0) {
-    const EVT_LDS ChainConst& k = chain_const(smem);
-    bool ok = false;
-    for (unsigned i = 0; i < k.spin; ++i) {
-      if (__hip_atomic_load(k.cnt + tm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= k.need) {
-        ok = true;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    if (!ok) __hip_atomic_store(k.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const unsigned d = __hip_atomic_load(k.gdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *(EVT_LDS int*)(smem + CHAIN_WORD) = (d >= k.totalA) ? 1 : 0;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    wait_vmcnt0();
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  big8_bar();
-  cx.all_ready = __builtin_amdgcn_readfirstlane(*(const EVT_LDS int*)(smem + CHAIN_WORD)) != 0;
 }
 
 // Logical walk index -> output tile of the persistent 256 x 256 kernel. Walk index t of round
@@ -2013,36 +1621,24 @@ __device__ __forceinline__ bool pers_tile(int t, int G, int ntiles, int xgroups,
   return j < total / xgroups;
 }
 
-// The persistent tile walk of one GEMM from logical tile `tile`: in steps of gridDim.x (ROLE 0, a
-// plain launch), or the block's dequeued walk indices (chained launch, ChainCtx): ROLE bit 1 =
-// producer (outputs write-through; a tile's panel is published at the block's next epilogue,
-// after every wave's vmcnt(0) drain and a barrier, the last one after the loop's drain), bit 2 =
-// consumer (each tile's prologue waits for its panel).
-template <int FL, int DBG, bool PADN, int ROLE, typename P = GemmParams>
-__device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* smem,
-                                         ChainCtx& cx) {
+// The persistent tile walk of one GEMM from logical tile `tile` in steps of gridDim.x.
+template <int FL, int DBG, bool PADN, typename P = GemmParams>
+__device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* smem) {
   // a quarter of the residual before the last K-tile (out-proj 160 -> 153 us); DBG 20: A/B without
-  // (PERS_RIA: none, the main loop adds the residual)
-  constexpr bool RIA = (FL & PERS_RIA) != 0;
-  static_assert(!RIA || ((FL & EPI_RESID) != 0 && (FL & EPI_POS) == 0 && ROLE == 0 && DBG == 0),
-                "residual chunks: standalone persistent residual GEMMs (gemm_chain_launch)");
-  constexpr int ER = ((FL & EPI_RESID) != 0 && !RIA && DBG != 7 && DBG != 20 && DBG != 18)
+  constexpr int ER = ((FL & EPI_RESID) != 0 && DBG != 7 && DBG != 20 && DBG != 18)
                          ? (DBG == 21 ? 1 : 2) : 0;  // DBG 21: A/B with one quarter
-  constexpr bool SC1 = (ROLE & 1) != 0;
-  constexpr bool WAITS = (ROLE & 2) != 0;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const int G = gridDim.x;
   const int nk = p.K / 64;
-  const int xg = ROLE == 0 ? p.xgroups : 0;
+  const int xg = p.xgroups;
   int tm, tn;
   pers_tile(tile, G, p.ntiles, xg, total, tm, tn);
   if (DBG == 5) {  // experiment: stagger the blocks' start
     const int q = (blockIdx.x >> 3) & 3;
     for (int i = 0; i < q * nk; ++i) __builtin_amdgcn_s_sleep(20);
   }
-  if constexpr (WAITS) chain_wait(cx, tm, smem);
   pers_coop_dma<FL>(p, smem, wave, lane, tm * BIG_BM, tn * BIG_BN);
   big8_prologue(p, smem, wave, lane, tm * BIG_BM, tn * BIG_BN, nk);
   wait_vmcnt0();  // the first K-tile's waits assume PERS_X younger VMEM ops or a drain
@@ -2050,7 +1646,6 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
   // nk >= 3: per-tile LayerNorm coefficients / next statistics DMA inside the main loop
   const bool early = nk >= 3 && DBG != 16 && DBG != 17;
   int iter = 0;
-  int pub_tm = -1;  // ROLE 1: the previous tile's panel, published during this tile
   auto stamp = [&](int k) {  // DBG 3: timeline of block's tiles (s_memtime, wave 0)
     if ((DBG == 3 || DBG == 5) && tid == 0 && iter < 16)
       ((unsigned long long*)p.pos)[((int64_t)blockIdx.x * 16 + iter) * 8 + k] = __builtin_amdgcn_s_memtime();
@@ -2058,11 +1653,6 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
   while (true) {
     const int m0 = tm * BIG_BM, n0 = tn * BIG_BN;
     stamp(0);
-    if constexpr (ROLE != 0) {
-      // the ticket naming the block's tile after `next` (read after the epilogue: by then this
-      // wave's K-tile-1 waits have retired it, vmcnt counting in issue order)
-      if (tid == 0) chain_take_ticket(cx, smem);
-    }
     f32x4 acc[4][8];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -2071,15 +1661,13 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
     int ln = lane;
     asm volatile("" : "+v"(ln));  // per-tile lane addresses: not hoisted out of the tile loop
     u32x4 rre[2][4];  // ER: residual row pair 0 loaded before the last K-tile
-    const int next = ROLE == 0 ? tile + G : cx.nxt - cx.base;
+    const int next = tile + G;
     int ntm = 0, ntn = 0;
-    const bool has_next = next >= 0 && pers_tile(next, G, p.ntiles, xg, total, ntm, ntn);
+    const bool has_next = pers_tile(next, G, p.ntiles, xg, total, ntm, ntn);
     if (!has_next) ntm = ntn = 0;
-    // consumer: the next tile's operands may be fetched ahead only once every panel is known ready
-    const bool rdy = !WAITS || cx.all_ready;
     // the next tile's prologue rides in the last K-tiles' idle DMA slots (big8_ktile) as K-tiles
     // nk, nk + 1 of one stream: for odd nk the next tile starts at the other buffer parity
-    const bool cont = has_next && rdy && nk >= 2 && DBG != 16 && (DBG != 6 || !(nk & 1));
+    const bool cont = has_next && nk >= 2 && DBG != 16 && (DBG != 6 || !(nk & 1));
     const int npar = cont ? par ^ (nk & 1) : 0;
     auto last = [&]() {
       if constexpr (ER > 0) pers_resid_early<0, 1>(p, wm, wn, ln, m0, n0, rre);
@@ -2087,63 +1675,33 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
     auto last3 = [&]() {  // row pair 1 once the n-half-1 fragments are dead (phase 3)
       if constexpr (ER > 1) pers_resid_early<1, 2>(p, wm, wn, ln, m0, n0, rre);
     };
-    // residual tile pulled into L2 EVT_RES_PF K-tiles before the epilogue: two 4-B DMAs per lane
-    // (into a dead LDS sink) touch its 1024 128-B lines, so the epilogue's residual loads, which
-    // all 256 CUs issue at the same time, hit L2 instead of queueing at HBM
-    auto pf = [&]() {  // the rows the early residual loads (ER) do not cover: wm 128 + 64 .. 127
-      const int L = wave * 64 + ln;  // line: row r = L >> 2, 128-B segment L & 3
-      const int r = L >> 2;
-      const int gm = min(m0 + (r >> 6) * 128 + 64 + (r & 63), p.M - 1);
-      const int gn = min(n0 + (L & 3) * 64, p.N - 2);
-      __builtin_amdgcn_global_load_lds((const bf16*)p.resid + (int64_t)gm * p.ldr + gn,
-                                       (EVT_LDS char*)smem + PERS_SINK, 4, 0, 0);
-    };
-    constexpr int PFX = ((FL & EPI_RESID) != 0 && !RIA && EVT_RES_PF > 0) ? 1 : 0;
-    auto make_rh = [&]() {
-      if constexpr (RIA) return RiaHook<FL>(p, smem, wm, wn, ln, m0, n0);
-      else return NoRh{};
-    };
-    auto rh = make_rh();
-    const int tpf = PFX ? nk - 1 - EVT_RES_PF : -1;
     if (early) {
       // this tile's LayerNorm coefficients by wave group 1 while it waits for group 0's first
       // phase; the next tile's statistics rows / column vectors DMA'd after K-tile 0 (PERS_RAW is
       // free once those coefficients are read: every later phase retires group 1's LDS ops)
       auto pre1 = [&]() { pers_coef<FL>(p, smem, tid - 256); };
       auto mid = [&]() {
-        if (has_next && rdy) pers_coop_dma<FL>(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN);
+        if (has_next) pers_coop_dma<FL>(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN);
       };
       if constexpr (DBG == 18)  // A/B: groups re-synchronised before the epilogue
         big8_loop<PERS_X>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
                           ntn * BIG_BN, pre1, mid, {}, {}, par);
       else
         big8_loop<PERS_X, true, decltype(pre1), decltype(mid), (ER > 0 ? 4 : 0), decltype(last),
-                  (ER > 1 ? 4 : 0), decltype(last3), P, PFX, decltype(pf)>(
+                  (ER > 1 ? 4 : 0), decltype(last3), P>(
             p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM, ntn * BIG_BN, pre1, mid,
-            last, last3, par, pf, tpf, &rh);
+            last, last3, par);
       stamp(1);
-      if (has_next && !cont) {
-        if constexpr (WAITS) {
-          if (!rdy) {  // before every panel is known ready: wait, then the skipped DMAs
-            chain_wait(cx, ntm, smem);
-            pers_coop_dma<FL>(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN);
-          }
-        }
-        big8_prologue(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nk);
-      }
+      if (has_next && !cont) big8_prologue(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nk);
     } else {
       big8_loop<PERS_X, false, NoOp, NoOp, (ER > 0 ? 4 : 0), decltype(last), (ER > 1 ? 4 : 0),
-                decltype(last3), P, PFX, decltype(pf)>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk,
-                                                       cont, ntm * BIG_BM, ntn * BIG_BN, {}, {},
-                                                       last, last3, par, pf, tpf);
+                decltype(last3), P>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
+                                    ntn * BIG_BN, {}, {}, last, last3, par);
       stamp(1);
       pers_coef<FL>(p, smem, tid);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       big8_bar();
       if (has_next) {
-        if constexpr (WAITS) {
-          if (!rdy) chain_wait(cx, ntm, smem);
-        }
         pers_coop_dma<FL>(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN);
         if (!cont) big8_prologue(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nk);
       }
@@ -2151,33 +1709,12 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     stamp(2);
-    // producer: the previous tile's write-through stores and statistics must be complete in every
-    // wave before thread 0 publishes its panel. The counted K-tile-1 waits already imply it where
-    // vmcnt retires loads, stores and LDS-DMA in issue order (MI355X_MICROARCH.md); the compiler's
-    // model does not assume that ordering, so every wave also drains its vector-memory
-    // counter and the block meets at a barrier first. This drains the next tile's prologue DMAs
-    // once per tile: a cost on the opt-in chained path only (the separate launches publish nothing).
-    if constexpr ((ROLE & 1) != 0) {
-      if (pub_tm >= 0) {
-        wait_vmcnt0();
-        big8_bar();
-        if (tid == 0) chain_publish(smem, pub_tm);
-      }
-      pub_tm = tm;
-    }
     const bool interior = (m0 + BIG_BM <= p.M) && (n0 + BIG_BN <= p.N);
     if constexpr (DBG == 6)  // A/B: the round-1 epilogue
       pers_epilogue_v1<FL, 0, PADN>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior);
     else
-      pers_epilogue<FL, DBG, PADN, ER, SC1>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior,
-                                            iter, rre, npar);
-    if constexpr (ROLE != 0) {  // broadcast the ticket: the block's tile after `next`
-      if (tid == 0) *(EVT_LDS unsigned*)(smem + CHAIN_TICKET) = cx.tk;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      big8_bar();
-      cx.cur = cx.nxt;
-      cx.nxt = (int)__builtin_amdgcn_readfirstlane(*(const EVT_LDS unsigned*)(smem + CHAIN_TICKET));
-    }
+      pers_epilogue<FL, DBG, PADN, ER>(p, smem, acc, wave, wm, wn, m0, n0, tn, lane, interior,
+                                       iter, rre, npar);
     stamp(7);
     ++iter;
     if (!has_next) break;
@@ -2186,11 +1723,6 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
     tile = next;
     tm = ntm;
     tn = ntn;
-  }
-  if constexpr ((ROLE & 1) != 0) {  // the last tile: drain every wave, then publish
-    wait_vmcnt0();
-    big8_bar();
-    if (tid == 0) chain_publish(smem, pub_tm);
   }
 }
 
@@ -2203,17 +1735,16 @@ __global__ __launch_bounds__(512, 2) void gemm_pers_kernel(GemmParams p, int tot
     int tm, tn;
     if (!pers_tile(tile, G, p.ntiles, p.xgroups, total, tm, tn)) return;
   }
-  ChainCtx cx;
   if constexpr ((FL & EPI_GATHER) != 0) {
     MergeParams q;
     static_cast<GemmParams&>(q) = p;
-    pers_run<FL, DBG, PADN, 0>(q, total, tile, smem, cx);
+    pers_run<FL, DBG, PADN>(q, total, tile, smem);
   } else if constexpr ((FL & EPI_SPLIT) != 0) {
     UnfoldParams q;
     static_cast<GemmParams&>(q) = p;
-    pers_run<FL, DBG, PADN, 0>(q, total, tile, smem, cx);
+    pers_run<FL, DBG, PADN>(q, total, tile, smem);
   } else {
-    pers_run<FL, DBG, PADN, 0>(p, total, tile, smem, cx);
+    pers_run<FL, DBG, PADN>(p, total, tile, smem);
   }
 }
 
@@ -2583,63 +2114,6 @@ __global__ __launch_bounds__(512, 2) void gemm_p384_kernel(GemmParams p, int tot
   p3_run<FL>(q, total, tile, smem);
 }
 
-// Two dependent GEMMs in one persistent launch: producer FA (out-proj: LN residual, row
-// statistics) over every M panel, then consumer FB (FC1: LN-folded A = the producer's output) in
-// the same tile walk, so the CUs the producer's last, partial tile round
-// leaves idle start consumer tiles of panels that are already done (per-panel hand-off, acquire
-// at the consumer; DESIGN.md "Chained GEMM launches"). Tiles are dequeued in walk order (ChainCtx):
-// progress needs no co-residency; waits are bounded and a timeout is reported through `err`.
-// sync: [panels] counters, gdone, head, fin (zero at allocation, zeroed again by the last block).
-template <int FA, int FB>
-__global__ __launch_bounds__(512, 2) void gemm_chain_kernel(GemmParams pa, GemmParams pb,
-                                                            int totalA, int totalB,
-                                                            unsigned* sync, unsigned* err,
-                                                            unsigned spin) {
-  __shared__ __attribute__((aligned(16))) char smem[CHAIN_LDS_ALL];
-  const int G = gridDim.x;
-  const int panels = (pa.M + BIG_BM - 1) / BIG_BM;
-  ChainCtx cx;
-  // the block's first two tiles (consecutive walk indices) and the launch constants
-  if (threadIdx.x == 0) {
-    EVT_LDS ChainConst& k = *(EVT_LDS ChainConst*)(smem + CHAIN_CONST);
-    k.cnt = sync;
-    k.gdone = sync + panels;
-    k.head = sync + panels + 1;
-    k.err = err;
-    k.need = (unsigned)pa.ntiles;
-    k.totalA = (unsigned)totalA;
-    k.total = (unsigned)(totalA + totalB);
-    k.spin = spin;
-    const unsigned w0 = __hip_atomic_fetch_add(sync + panels + 1, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *(EVT_LDS unsigned*)(smem + CHAIN_TICKET) = w0;
-  }
-  __syncthreads();
-  cx.cur = (int)__builtin_amdgcn_readfirstlane(*(const EVT_LDS unsigned*)(smem + CHAIN_TICKET));
-  cx.nxt = cx.cur + 1;
-  if (cx.cur < totalA) {
-    cx.base = 0;
-    pers_run<FA, 0, false, 1>(pa, totalA, cx.cur, smem, cx);
-  }
-  if (cx.cur >= totalA && cx.cur < totalA + totalB) {
-    cx.base = totalA;
-    pers_run<FB, 0, false, 2>(pb, totalB, cx.cur - totalA, smem, cx);
-  }
-  // self-cleaning hand-off words: the last block to finish (every other block is past its last
-  // poll and dequeue) zeroes them for the next chained launch
-  unsigned* fin = sync + panels + 2;
-  if (threadIdx.x == 0) {
-    wait_vmcnt0();
-    const unsigned old = __hip_atomic_fetch_add(fin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *(EVT_LDS unsigned*)(smem + CHAIN_WORD) = old == (unsigned)G - 1 ? 1u : 0u;
-  }
-  __syncthreads();
-  if (*(const EVT_LDS unsigned*)(smem + CHAIN_WORD)) {
-    for (int i = threadIdx.x; i < panels + 2; i += blockDim.x)
-      __hip_atomic_store(sync + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (threadIdx.x == 0) __hip_atomic_store(fin, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 // ---------------------------------------------------------------------------------------------
 // Stream-K persistent kernel. The persistent kernel above runs every CU through identical tiles
 // in lock step, so all 256 epilogues (32 MB of output stores, plus 32 MB of residual loads for
@@ -2843,8 +2317,7 @@ bool gemm_lab_pers_variant(int v) {
 
 bool use_pers(const GemmParams& p, int flags) {
   const int v = g_gemm_variant;
-  if (v != 0 && v != 9 && v != 16 && v != 31 && v != 32 && v != 33 && v != 34 && v != 35 &&
-      !gemm_lab_pers_variant(v))
+  if (v != 0 && v != 9 && v != 16 && v != 31 && !gemm_lab_pers_variant(v))
     return false;
   // timeline variants stamp s_memtime through p.pos: never on the patch GEMM (p.pos = the table)
   if ((v == 13 || v == 15) && (flags & EPI_POS)) return false;
@@ -2856,31 +2329,12 @@ bool use_pers(const GemmParams& p, int flags) {
   return true;
 }
 
-// (EVT_RIA lab builds) residual GEMMs with K >= 64 RIA_NK: the residual added by the main loop
-// (PERS_RIA); variant 33 keeps the epilogue residual (A/B in one process)
-template <int FL>
-bool launch_pers_ria(const GemmParams& q, int G, int total, hipStream_t s) {
-  if constexpr (EVT_RIA && (FL & EPI_RESID) != 0 && (FL & (EPI_POS | EPI_GATHER | EPI_SPLIT)) == 0) {
-    if (g_gemm_variant == 33 || q.K % 64 || q.K / 64 < RIA_NK) return false;
-    if (q.N % BIG_BN == 0)
-      hipLaunchKernelGGL((gemm_pers_kernel<FL | PERS_RIA, 0, false>), dim3(G), dim3(512), 0, s, q,
-                         total);
-    else
-      hipLaunchKernelGGL((gemm_pers_kernel<FL | PERS_RIA>), dim3(G), dim3(512), 0, s, q, total);
-    return true;
-  } else {
-    (void)q, (void)G, (void)total, (void)s;
-    return false;
-  }
-}
-
 // XCD groups of the persistent walk (pers_tile): 2 where the weight panels split evenly over
 // two groups of four XCDs and the launch has more than one round (FC1 of the D = 768 models: 12
-// panels -> 6 per group); variant 34 keeps one group, 35 asks for 4 (A/B)
+// panels -> 6 per group; measured round 4: one group 484.5 us, two 479.9, four 479.3 per FC1 launch)
 int pers_xgroups(int ntiles, int G, int total) {
   if (G != 256 || total <= G) return 1;  // the walk arithmetic assumes 8 XCDs of 32 blocks
-  const int want = g_gemm_variant == 34 ? 1 : g_gemm_variant == 35 ? 4 : 2;
-  return (ntiles % want == 0 && ntiles / want >= 3) ? want : 1;
+  return (ntiles % 2 == 0 && ntiles / 2 >= 3) ? 2 : 1;
 }
 
 template <int FL>
@@ -2921,8 +2375,6 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_pers_kernel<(FL & ~(EPI_GELU | EPI_GELU_ERF)), 0, false>), dim3(G),
                        dim3(512), 0, s, q, total);
 #endif
-  else if (launch_pers_ria<FL>(q, G, total, s))
-    ;
   else if (p.N % BIG_BN == 0)
     hipLaunchKernelGGL((gemm_pers_kernel<FL, 0, false>), dim3(G), dim3(512), 0, s, q, total);
   else
@@ -2957,25 +2409,6 @@ hipError_t launch_p384(const GemmParams& p, hipStream_t s) {
   int G = min(total, num_cus());
   if (G >= 8 && total > G) G &= ~7;
   hipLaunchKernelGGL((gemm_p384_kernel<FL>), dim3(G), dim3(512), 0, s, q, total);
-  return hipGetLastError();
-}
-
-// Chained producer -> consumer launch (gemm_chain_kernel). hipErrorNotSupported when the pair
-// does not qualify (the caller then launches the two GEMMs separately).
-template <int FA, int FB>
-hipError_t launch_chain(const GemmParams& pa, const GemmParams& pb, const ChainWords& cw,
-                        hipStream_t s) {
-  GemmParams qa = pa, qb = pb;
-  qa.ntiles = (pa.ntiles * GEMM_BN) / BIG_BN;
-  qb.ntiles = (pb.ntiles * GEMM_BN) / BIG_BN;
-  const int panels = (pa.M + BIG_BM - 1) / BIG_BM;
-  const int totalA = panels * qa.ntiles, totalB = panels * qb.ntiles;
-  const int G = num_cus();  // one block per CU when resident; any residency is correct
-  // sync: [panels] counters, gdone, head, fin; zero at allocation, left zeroed by every launch
-  if (G < 1 || totalA < G || (size_t)(panels + 3) * 4 > cw.sync_bytes || !cw.err)
-    return hipErrorNotSupported;
-  hipLaunchKernelGGL((gemm_chain_kernel<FA, FB>), dim3(G), dim3(512), 0, s, qa, qb, totalA, totalB,
-                     cw.sync, cw.err, cw.spin);
   return hipGetLastError();
 }
 
@@ -3164,7 +2597,6 @@ int device_cus() { return num_cus(); }
 void gemm_set_variant(int v) { g_gemm_variant = v; }
 bool gemm_variant_supported(int v) {
   return v == 0 || v == 1 || v == 2 || v == 6 || v == 8 || v == 9 || v == 16 || v == 30 || v == 31 ||
-         v == 32 || (EVT_RIA && v == 33) || v == 34 || v == 35 ||
          gemm_lab_pers_variant(v)
 #ifdef EVT_GEMM_LAB
          || v == 106 || v == 108
@@ -3178,48 +2610,6 @@ size_t gemm_sk_bytes() { return 4096 + (size_t)SK_MAX_G * SK_SLOT_FLOATS * sizeo
 void gemm_sk_bind(void* ws, GemmParams& p) {
   p.sk_flags = ws ? (int*)ws : nullptr;
   p.sk_part = ws ? (float*)((char*)ws + 4096) : nullptr;
-}
-
-hipError_t gemm_chain_launch(int dtype, int fa, const GemmParams& pa, int fb, const GemmParams& pb,
-                             const ChainWords& cw, hipStream_t s) {
-  constexpr int RES = EPI_BIAS | EPI_RESID | EPI_RESLN | EPI_STATS;
-  if (dtype != DT_BF16 || (g_gemm_variant != 0 && !(EVT_RIA && g_gemm_variant == 33)) || fa != RES ||
-      !cw.sync)
-    return hipErrorNotSupported;
-  // where the standalone out-proj adds its residual in the main loop (PERS_RIA) the pair runs
-  // separately: the producer's extra registers make hipcc spill the ticket atomic's destination
-  // VGPR before the atomic returns (an asm output; measured round 4: a broken tile walk), and a
-  // producer without PERS_RIA would not be bitwise the separate launches
-  if (EVT_RIA && g_gemm_variant == 0 && pa.K % 64 == 0 && pa.K / 64 >= RIA_NK)
-    return hipErrorNotSupported;
-  // only where both GEMMs would take the 256 x 256 persistent kernel on their own (bitwise the
-  // separate launches)
-  if (pa.M != pb.M || pa.N % BIG_BN || pb.N % BIG_BN || pa.K / 64 < 3 || pb.K / 64 < 3 ||
-      !use_big(pa, fa) || !use_big(pb, fb) || !use_pers(pa, fa) || !use_pers(pb, fb) ||
-      use_p384(pa, fa) || use_p384(pb, fb))
-    return hipErrorNotSupported;
-  if (fb == (EPI_LNIN | EPI_BIAS | EPI_GELU))
-    return launch_chain<RES, EPI_LNIN | EPI_BIAS | EPI_GELU>(pa, pb, cw, s);
-  return hipErrorNotSupported;
-}
-
-// Diagnostics: `blocks` workgroups that each hold a whole CU (all 160 KiB of LDS) for `usec`
-// microseconds (s_memrealtime, 100 MHz), sleeping: the uneven-load condition of the chained-launch
-// tests (another stream's kernel keeps CUs while a forward runs).
-__global__ __launch_bounds__(64) void occupy_kernel(unsigned long long ticks, int* sink) {
-  __shared__ int hold[160 * 1024 / 4];
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
-  hold[threadIdx.x] = (int)threadIdx.x;
-  __syncthreads();
-  if (hold[63 - threadIdx.x] == -1) sink[0] = 1;  // never: keeps the LDS allocation
-}
-
-hipError_t occupy_launch(int blocks, int usec, hipStream_t s) {
-  if (blocks <= 0 || usec < 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(occupy_kernel, dim3(blocks), dim3(64), 0, s,
-                     (unsigned long long)usec * 100ull, (int*)nullptr);
-  return hipGetLastError();
 }
 
 hipError_t gemm_launch(int dtype, int flags, const GemmParams& p, hipStream_t s) {

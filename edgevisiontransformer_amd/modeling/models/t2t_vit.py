@@ -86,18 +86,6 @@ class T2T_ViT:
                                           ctypes.byref(out)))
         self._handle = out.value
         self._max_batch = max_batch
-        if getattr(self, "_fusion", None) is not None:
-            _lib.check(lib.evt_model_set_fusion(ctypes.c_void_p(self._handle), self._fusion))
-
-    def set_fusion(self, flags: int) -> None:
-        """Fused-kernel switches of this model (evt_model_set_fusion; _lib.FUSE_QKV_ATTENTION:
-        LN1-folded QKV + attention as one kernel; _lib.FUSE_GEMM_CHAIN:
-        chained out-proj -> FC1 launches). Kept across re-plans for larger
-        batches."""
-        self._fusion = int(flags)
-        if self._handle:
-            _lib.check(_lib.load_library().evt_model_set_fusion(ctypes.c_void_p(self._handle),
-                                                                self._fusion))
 
     def workspace_bytes(self, batch: int) -> int:
         lib = _lib.load_library()

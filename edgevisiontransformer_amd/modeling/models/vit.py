@@ -155,36 +155,6 @@ class ViT:
                                           ctypes.byref(out)))
         self._handle = out.value
         self._max_batch = max_batch
-        if getattr(self, "_fusion", None) is not None:
-            _lib.check(lib.evt_model_set_fusion(ctypes.c_void_p(self._handle), self._fusion))
-        if getattr(self, "_chain_spin", None) is not None:
-            _lib.check(lib.evt_model_set_chain_spin(ctypes.c_void_p(self._handle), self._chain_spin))
-
-    def set_fusion(self, flags: int) -> None:
-        """Fused-kernel switches of this model (evt_model_set_fusion; _lib.FUSE_QKV_ATTENTION:
-        LN1-folded QKV + attention as one kernel; _lib.FUSE_GEMM_CHAIN:
-        chained out-proj -> FC1 launches). Kept across re-plans for larger
-        batches."""
-        self._fusion = int(flags)
-        if self._handle:
-            _lib.check(_lib.load_library().evt_model_set_fusion(ctypes.c_void_p(self._handle),
-                                                                self._fusion))
-
-    def check_status(self) -> None:
-        """Raise if a forward of this model that has completed since the last check failed on the
-        device (evt_model_status: a chained GEMM hand-off wait that timed out). Synchronise the
-        stream first to cover the forwards enqueued so far."""
-        if self._handle:
-            _lib.check(_lib.load_library().evt_model_status(ctypes.c_void_p(self._handle)))
-
-    def set_chain_spin(self, polls: int) -> None:
-        """Diagnostics (evt_model_set_chain_spin): poll bound of the chained launch's hand-off
-        waits; 0 makes them give up at once (the evt_model_status failure path), < 0 restores the
-        default. Applies to this handle only (re-applied after a re-plan for a larger batch)."""
-        self._chain_spin = int(polls)
-        if self._handle:
-            _lib.check(_lib.load_library().evt_model_set_chain_spin(ctypes.c_void_p(self._handle),
-                                                                    self._chain_spin))
 
     def workspace_bytes(self, batch: int) -> int:
         lib = _lib.load_library()
@@ -233,10 +203,8 @@ class ViT:
         logits = torch.empty((x.shape[0], c.num_classes), dtype=torch.float32, device=self.device)
         with torch.cuda.device(self.device):
             self.forward_into(x, logits)
-            # model(img) returns finished logits (as the reference's eager Keras call): wait for
-            # them and surface any device-side failure of this forward
-            torch.cuda.current_stream(self.device).synchronize()
-            self.check_status()
+        # stream-ordered, as every torch op: a numpy input gets numpy logits (.cpu() waits for
+        # them), a device tensor gets device logits without a host sync
         return logits.cpu().numpy() if was_numpy else logits
 
     call = __call__

@@ -135,7 +135,7 @@ enum {
   EVT_PROF_FC1 = 5,             /* LN2-folded Dense(M, gelu)            ffn.py:8 */
   EVT_PROF_FC2 = 6,             /* Dense(D) + LN2(xm) residual          ffn.py:9 */
   EVT_PROF_HEAD = 7,            /* mlp_head / classifier                vit.py:38-39,55 */
-  EVT_PROF_QKV_ATTENTION = 8,   /* fused QKV + attention (evt_model_set_fusion) */
+  /* 8: unused (the round-1..4 fused QKV + attention kernel, measured slower, removed) */
   EVT_PROF_T2T_UNFOLD = 9,      /* tf_Unfold soft splits 0-2            t2t_vit.py:7-40,66-81 */
   EVT_PROF_T2T_KQV = 10,        /* TokenPerformer LN1-folded kqv Dense  transformer_encoder.py:84 */
   EVT_PROF_T2T_PERFORMER = 11,  /* TokenPerformer core (prm_exp .. FFN) transformer_encoder.py:67-99 */
@@ -156,30 +156,6 @@ int evt_model_profile_read(evt_model* m, float* us, int* launches);
  * the reference's FLOP counter (flops_calculation.py:216-251) per kernel; bench.py divides by the
  * role's time for the MFMA and HBM roofline fractions. */
 int evt_model_profile_work(evt_model* m, double* gflop, double* gbytes);
-
-/* Fused-kernel switches of ONE model handle (default 0: none):
- * EVT_FUSE_QKV_ATTENTION runs each bf16 ViT layer's LN1-folded QKV Dense and attention core as
- * one kernel (evt_qkv_attention) where the token count allows. Opt-in: measured slower than the
- * separate kernels at DeiT-base bs512 ("Fused QKV + attention").
- * EVT_FUSE_GEMM_CHAIN runs each bf16 ViT layer's out-proj -> FC1 as one chained persistent launch
- * where the shapes allow (FC1 tiles start on the CUs the out-proj's last tile round leaves idle;
- * bitwise the same results; DESIGN.md, "Chained GEMM launches"). Tiles are dequeued in dependency
- * order, so the launch completes whatever other streams' kernels occupy; its hand-off waits are
- * bounded, and a wait that gives up is reported by evt_model_status (never a silent result).
- * Opt-in: with dequeued tiles it measured 0.9 % slower than the separate launches at DeiT-base
- * bs512.
- * Not used while the handle is profiling (evt_model_profile brackets one role per launch).
- * Takes effect at the next forward / graph capture of that handle; other handles are unaffected. */
-#define EVT_FUSE_QKV_ATTENTION 1
-#define EVT_FUSE_GEMM_CHAIN 2
-int evt_model_set_fusion(evt_model* m, int flags);
-
-/* Deferred device-side failures of the handle's forwards: EVT_EHIP (with evt_last_error) if a
- * forward that has COMPLETED since the last call hit a failure only the device can see (a chained
- * GEMM hand-off wait that timed out: that forward's logits are invalid), else EVT_OK; the report
- * is consumed. Synchronise the forward's stream first to cover a given forward; evt_vit_forward
- * and evt_graph_launch also return it (before enqueuing anything) for earlier forwards. */
-int evt_model_status(evt_model* m);
 
 /* Pack a Keras [K, N] fp32 kernel into the GEMM operand layout Wp[Npad][Kpad] (dtype), zero
  * padded, optionally scaling row k by row_scale[k] (a LayerNorm gamma folded into the weights;
@@ -240,17 +216,6 @@ int evt_dense(int dtype, const evt_dense_args* args, void* stream);
  * Reference: mlp_head `vit.py:38-39,55`. */
 int evt_dense_splitk(int dtype, const evt_dense_args* args, int splits, float* partials,
                      void* stream);
-
-/* Fused attention sublayer up to the out-projection (bf16 only): the LN1-folded QKV Dense
- * (norm.py:12 + attention.py:17,24) and the attention core (attention.py:20-34) in one kernel, q / k
- * / v never written to memory. x [B*N, D] the raw token stream (bf16, D % 64 == 0), stats
- * [B*N, 2*ceil(D/256), 2] its per-slab (sum, sum of squares) partials (any split over the slots),
- * Wp / colsum / cvec the packed gamma-folded Keras [D, 3*H*64] qkv kernel (evt_pack_weight with
- * row_scale = gamma, Kpad = D) and its fold vectors (evt_ln_fold with beta and the qkv bias or
- * NULL); out [B*N, ldo] columns (h d). 192 < N <= 208 (the 224/16 ViT token count 197). */
-int evt_qkv_attention(const void* x, int D, const float* stats, const void* Wp, const float* colsum,
-                      const float* cvec, int B, int N, int H, float scale, float eps, void* out,
-                      int64_t ldo, void* stream);
 
 /* Multi-head attention core (attention.py:20-34): qkv [B*N, ldq] with columns (qkv h d), head
  * size 64 -> out [B*N, ldo] columns (h d). N <= 256. */
@@ -460,26 +425,14 @@ int evt_attention_mx8(const void* qkv, int64_t ldq, void* q8, int64_t ldq8, uint
 
 /* GEMM kernel selection for bf16 Dense launches made FROM THE CALLING THREAD (thread-local: other
  * threads and their handles are unaffected), for parity tests and A/B measurements only:
- * 0 = automatic (256x256 tiles when the problem has >= 256 of them, the tile-persistent kernel
- * for the fused epilogues, else 128x128), 1 = always 128x128, 2 / 6 / 8 = non-persistent 256x256
- * tiles with the plain / interleaved / 8-phase ping-pong main loop whenever the packed width
- * allows, 9 = tile-persistent, 16 = stream-K persistent where it applies, 30 = the 128 x 384
- * persistent tiles wherever the width allows (multiple of 384), 31 = automatic without them, 32 =
- * automatic with the round-3 tile rule (256 x 256 tiles only from 256 of them up), 34 / 35 =
- * automatic with the persistent walk's weight panels split over 1 / 4 XCD groups (the default
- * splits them over 2 where they divide evenly; outputs are bitwise the same). Builds with
+ * 0 = automatic (the persistent 256x256 kernel unless its tile rounds cost more than the 128x128
+ * kernel's, else 128x128), 1 = always 128x128, 2 / 6 / 8 = non-persistent 256x256 tiles with the
+ * plain / interleaved / 8-phase ping-pong main loop whenever the packed width allows, 9 =
+ * tile-persistent, 16 = stream-K persistent where it applies, 30 = the 128 x 384 persistent tiles
+ * wherever the width allows (multiple of 384), 31 = automatic without them. Builds with
  * EVT_LAB=1 (-DEVT_GEMM_LAB) also accept the ablation / timeline variants 10, 11, 13, 15, 17-25,
  * 106, 108; other values return EVT_EINVAL. */
 int evt_set_gemm_variant(int variant);
-
-/* Poll bound of the handle's chained-launch hand-off waits (~0.1 us per poll; default 2^23,
- * a negative value restores it). 0 makes every first wait of a block give up at once: the
- * failure-reporting path of evt_model_status, for tests. */
-int evt_model_set_chain_spin(evt_model* m, int64_t polls);
-
-/* Launch `blocks` workgroups on `stream` that each hold a whole CU (all 160 KiB of its LDS) for
- * `usec` microseconds: uneven-load conditions for the chained-launch tests. */
-int evt_diag_occupy(int blocks, int usec, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,5 +1,5 @@
 """Per-role HBM traffic of a bench.py configuration from two rocprofv3 PMC passes (FETCH_SIZE,
-WRITE_SIZE; scripts/gpu_r4_pmc.sh) over real forwards (bench.py --no-probe).
+WRITE_SIZE; scripts/gpu_run.sh pmc:...) over real forwards (bench.py --no-probe).
 
     python scripts/pmc_roles.py <root with FETCH_SIZE/ WRITE_SIZE/> <model> <dtype> <batch> <role>
 

@@ -194,12 +194,3 @@ def dense_mx8(flags, Aq, As, wq, ws, kpad, npad, M, N, bias=None, resid=None, rs
     return (C, Cs) if Cs is not None else C
 
 
-def qkv_attention(x, stats, wp, colsum, cvec, B, N, H, scale=0.125, eps=1e-5, out=None):
-    """Fused LN1-folded QKV + attention (bf16): x [B*N, D] raw stream, stats its slab partials."""
-    D = x.shape[1]
-    if out is None:
-        out = torch.zeros((B * N, H * 64), dtype=torch.bfloat16, device=x.device)
-    _lib.check(_lib.load_library().evt_qkv_attention(_p(x), D, _p(stats), _p(wp), _p(colsum),
-                                                     _p(cvec), B, N, H, scale, eps, _p(out),
-                                                     out.stride(0), _s()))
-    return out

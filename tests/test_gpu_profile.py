@@ -12,23 +12,18 @@ from edgevisiontransformer_amd.profiling import kernel_times
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("fusion", [0, 1])
-def test_profile_roles_deit_tiny(gpu, fusion):
+def test_profile_roles_deit_tiny(gpu):
     from edgevisiontransformer_amd.modeling.models.vit import build_named
     m = build_named("deit_tiny", dtype="bf16", seed=0, max_batch=8)
     img = torch.randn((8, 3, 224, 224), device=gpu)
     logits = torch.empty((8, 1000), device=gpu)
-    m.set_fusion(fusion)
     kernel_times(m, img, logits, forwards=1)  # warm-up (event pool)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     kt = kernel_times(m, img, logits, forwards=3)
     wall_us = (time.perf_counter() - t0) / 3 * 1e6  # per profiled forward (+ one extra)
-    expect = {"patchify": 1, "patch_embed": 1, "out_proj": 12, "fc1": 12, "fc2": 12, "head": 1}
-    if fusion:
-        expect["qkv_attention"] = 12
-    else:
-        expect.update(qkv=12, attention=12)
+    expect = {"patchify": 1, "patch_embed": 1, "qkv": 12, "attention": 12, "out_proj": 12,
+              "fc1": 12, "fc2": 12, "head": 1}
     assert {k: v["launches"] for k, v in kt.items()} == expect
     assert all(v["us_per_launch"] > 0 for v in kt.values())
     # the bracketed intervals are disjoint and in stream order: their sum fits in the wall time

@@ -51,6 +51,9 @@ def test_hf_and_timm_state_dict_mapping():
         assert np.array_equal(back[k], params[k]), k
 
 
+BF16_ABS_GATE = {"std_small4_b3": 3.3e-2}
+
+
 def _cos_rows(a, b):
     return (a * b).sum(1) / (np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1))
 
@@ -70,5 +73,9 @@ def test_std_vit_gpu(gpu, name, dtype):
     if dtype == "f32":
         assert err <= 1e-3, err
     else:
-        assert err <= 3e-2 * max(1.0, float(np.abs(z["logits"]).max()) / 3.0), err
+        # the absolute bf16 gate (3e-2), except std_small4_b3 whose error is PINNED at its measured
+        # value (3.1e-2 since round 4's tile rule: 4 layers of D = 384, logits up to 4.3) so that
+        # any further drift fails; beside it a relative gate (1 % of the largest golden logit)
+        assert err <= BF16_ABS_GATE.get(name, 3e-2), err
+        assert err <= 1e-2 * float(np.abs(z["logits"]).max()), err
         assert _cos_rows(out, z["logits"]).min() >= 0.9995
