@@ -10,6 +10,7 @@
 #   bench:<args>            one bench.py line (e.g. bench:--batch,64,--steps,50)
 #   ab:<args>               alternating A/B of bench.py <args> over the arms in $ARMS, $ROUNDS times;
 #                           an arm is "lib=<path>" (EVT_LIB), "var=<n>" (--gemm-variant) or "base"
+#                           (PROBE=1: with the per-role probe; ROLES="attention qkv": print those roles)
 #   kstats:<args>           rocprofv3 kernel trace + stats of bench.py <args> -> <name>_kstats.txt
 #   pmc:<name>:<role>:<args>  FETCH_SIZE / WRITE_SIZE passes over real forwards -> pmc_<name>.json
 #   kpmc:<kernel>:<args>    SQ / TA / TD / TCP / TCC / GRBM counter passes of one kernel
@@ -19,7 +20,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${TAG:-run}
 mkdir -p $O
 ROUNDS=${ROUNDS:-2}
-summ() { python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); r=d['roofline'] or {}; print(sys.argv[2], d['config'].get('model'), 'bs', d['config'].get('per_gpu_batch'), d['value'], 'img/s', d['ms_per_step'], 'ms', 'model', d['model_roofline']['frac'], 'dom', r.get('role'), r.get('frac'), 'cpu', (d['cpu_baseline'] or {}).get('value'))" "$1" "$2"; }
+summ() { python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); r=d['roofline'] or {}; pr=r.get('per_role') or {}; print(sys.argv[2], d['config'].get('model'), 'bs', d['config'].get('per_gpu_batch'), d['value'], 'img/s', d['ms_per_step'], 'ms', 'model', d['model_roofline']['frac'], 'dom', r.get('role'), r.get('frac'), 'cpu', (d['cpu_baseline'] or {}).get('value'), ' '.join('%s=%.1f' % (k, v['us_per_launch']) for k, v in pr.items() if k in (sys.argv[3:] or ())))" "$1" "$2" ${ROLES:-}; }
 name_of() { echo "$1" | tr -c 'A-Za-z0-9_\n' '_' | sed 's/__*/_/g; s/^_//; s/_$//' | cut -c1-60; }
 for STEP in "$@"; do
   kind=${STEP%%:*}; rest=${STEP#*:}; [ "$rest" = "$STEP" ] && rest=""
@@ -36,12 +37,12 @@ for STEP in "$@"; do
     timeout -k 10 400 python bench.py $a > $O/$n.jsonl 2>&1 || { tail -5 $O/$n.jsonl; exit 1; }
     summ $O/$n.jsonl "$n" ;;
   ab)
-    a=${rest//,/ }
+    a=${rest//,/ }; np=--no-probe; [ -n "${PROBE:-}" ] && np=""
     for i in $(seq $ROUNDS); do
       for arm in ${ARMS:-base}; do
         n=$(name_of "ab $a $arm $i"); extra=""; envl=""
         case $arm in lib=*) envl="EVT_LIB=$R/${arm#lib=}";; var=*) extra="--gemm-variant ${arm#var=}";; esac
-        env $envl timeout -k 10 300 python bench.py $a $extra --cpu-seconds 0 --no-probe > $O/$n.jsonl 2>&1 || { tail -5 $O/$n.jsonl; exit 1; }
+        env $envl timeout -k 10 300 python bench.py $a $extra --cpu-seconds 0 $np > $O/$n.jsonl 2>&1 || { tail -5 $O/$n.jsonl; exit 1; }
         summ $O/$n.jsonl "$arm#$i"
       done
     done ;;
