@@ -868,7 +868,12 @@ hipError_t performer_launch(int dtype, const void* kqv, int64_t ldq, int B, int 
   if (kqv_perm && (ldq & 7)) return hipErrorInvalidValue;  // 16-B row pieces
   const int nchunk = performer_chunks(ntok);
   const int chunk = (ntok + nchunk - 1) / nchunk;
-  const int span = 512;  // tokens per output workgroup
+  // tokens per output workgroup: the images' token ranges cut into about one round of
+  // workgroups at 4 per CU (T2T-ViT-14 bs256: 3136 tokens -> 4 x 784, 784 -> 4 x 208: 1024
+  // workgroups each; a fixed 512 gave 1792 = 1.75 rounds and 512 = half a round). A token's
+  // arithmetic does not depend on its workgroup (bitwise the same for every span).
+  const int per_img = max(1, (4 * device_cus() + B - 1) / B);
+  const int span = max(64, ((ntok + per_img - 1) / per_img + 15) & ~15);
   if (dtype != DT_BF16)
     return performer_t<float>(kqv, ldq, B, ntok, chunk, nchunk, part, w, span, out, ldo, s, nullptr);
   return kqv_perm
