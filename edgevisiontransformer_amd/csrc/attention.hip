@@ -217,12 +217,12 @@ __device__ __forceinline__ void attn_stage_bf16(const AttnParams& p, EVT_LDS cha
                                                 EVT_LDS char* Vs, u32x4 (&qf)[NQW][2], int b,
                                                 int h, int wave, int lane) {
   constexpr int NP = NKT * 16, ROWB = 128;
-  const bf16* qkv = (const bf16*)p.qkv + (int64_t)b * p.N * p.ldq;
+  const bf16* qkv = (const bf16*)p.qkv + b * p.sb + h * p.sh;  // the (image, head) slice
   const int g = lane >> 4, c16 = lane & 15;
 #pragma unroll
   for (int i = 0; i < NQW; ++i) {
     const int qi = min((wave + WAVES * i) * 16 + c16, p.N - 1);
-    const bf16* qrow = qkv + (int64_t)qi * p.ldq + h * 64;
+    const bf16* qrow = qkv + (int64_t)qi * p.ldq;
     if (NTQ) {
       qf[i][0] = __builtin_nontemporal_load((const u32x4*)(qrow + 8 * g));
       qf[i][1] = __builtin_nontemporal_load((const u32x4*)(qrow + 8 * (g + 4)));
@@ -237,11 +237,11 @@ __device__ __forceinline__ void attn_stage_bf16(const AttnParams& p, EVT_LDS cha
     const int gr = min(row, p.N - 1);
     const bf16* rp = qkv + (int64_t)gr * p.ldq + ((sslot ^ srow) * 8);
     if (NT) {
-      __builtin_amdgcn_global_load_lds(rp + (p.H + h) * 64, Ks + i * 8 * ROWB, 16, 0, 2);
-      __builtin_amdgcn_global_load_lds(rp + (2 * p.H + h) * 64, Vs + i * 8 * ROWB, 16, 0, 2);
+      __builtin_amdgcn_global_load_lds(rp + p.ko, Ks + i * 8 * ROWB, 16, 0, 2);
+      __builtin_amdgcn_global_load_lds(rp + p.vo, Vs + i * 8 * ROWB, 16, 0, 2);
     } else {
-      glds16(rp + (p.H + h) * 64, Ks + i * 8 * ROWB);
-      glds16(rp + (2 * p.H + h) * 64, Vs + i * 8 * ROWB);
+      glds16(rp + p.ko, Ks + i * 8 * ROWB);
+      glds16(rp + p.vo, Vs + i * 8 * ROWB);
     }
   }
 }
@@ -669,9 +669,22 @@ void set_lds_attrs() {
 
 }  // namespace
 
-hipError_t attention_launch(int dtype, const AttnParams& p, hipStream_t s) {
-  if (p.B <= 0) return hipSuccess;
-  if (p.N <= 0 || p.N > 256 || p.H <= 0 || p.hd <= 0 || p.hd > 128) return hipErrorInvalidValue;
+hipError_t attention_launch(int dtype, const AttnParams& p_in, hipStream_t s) {
+  if (p_in.B <= 0) return hipSuccess;
+  if (p_in.N <= 0 || p_in.N > 256 || p_in.H <= 0 || p_in.hd <= 0 || p_in.hd > 128)
+    return hipErrorInvalidValue;
+  AttnParams p = p_in;
+  const bool strided = p.sb || p.sh || p.ko || p.vo;
+  if (strided) {  // an explicit slice layout: the bf16 h_k = 64 kernels only, 16-B aligned pieces
+    if (dtype != DT_BF16 || p.hd != 64 || p.q8 || p.sb % 8 || p.sh % 8 || p.ldq % 8 || p.ko % 8 ||
+        p.vo % 8 || p.ldq < 64 || p.ko < 0 || p.vo < 0 || p.sb < 0 || p.sh < 0)
+      return hipErrorInvalidValue;
+  } else {
+    p.sb = (int64_t)p.N * p.ldq;
+    p.sh = 64;
+    p.ko = p.H * 64;
+    p.vo = 2 * p.H * 64;
+  }
   if (p.hd != 64) {  // any other head size: the generic kernels (MX8 output: head size 64 only)
     if (p.q8) return hipErrorInvalidValue;
     return attention_gen_launch(dtype, p, s);

@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -101,10 +102,19 @@ struct SwinStage {
   std::vector<SwinBlock> blocks;
 };
 
+// EVT_QKV_LAYOUT=token (read when a model is created): keep the token-major qkv layout
+static bool qkv_headmajor_default() {
+  const char* e = std::getenv("EVT_QKV_LAYOUT");
+  return !(e && std::strcmp(e, "token") == 0);
+}
+
 struct evt_model {
   int family = 0;            // 0: ViT / ViT_Pruned, 1: T2T-ViT, 2: Swin
   bool standard = false;     // ViT with EVT_VIT_STANDARD semantics
   bool mx8 = false;          // EVT_DTYPE_MX8: MXFP8 encoder Dense layers (dtype is then bf16)
+  // QKV output head-major where the GEMM supports it (run_encoder); EVT_QKV_LAYOUT=token at model
+  // creation keeps the token-major layout (the A/B and bitwise-equality tests)
+  bool headmajor = qkv_headmajor_default();
   bool patch_cm = false;     // ViT: channel-major patch vectors / patch weight rows
   void* qa = nullptr;        // MX8: [rows][max(Dpad, innerpad)] e4m3 A operand (LN out / attn out)
   uint32_t* sa = nullptr;    // MX8: its scales [pad/128][rows]
@@ -523,12 +533,26 @@ int run_encoder(evt_model* m, int B, hipStream_t s) {
   const float log2e = 1.4426950408889634f;
   for (const Layer& L : m->layers) {
     const float scale_log2 = log2e / std::sqrt((float)L.hd);  // h_k^-0.5 (attention.py:13)
+    // qkv head-major ([B][heads][q | k | v][T][64], EPI_HM) where the QKV GEMM takes the
+    // persistent kernel (h_k = 64, bf16): an (image, head)'s q, k and v are three contiguous 25 KB
+    // runs instead of T 128-B pieces at a 3 D-element stride each; token-major otherwise
+    bool hm = false;
     {  // LN1-folded QKV (attention.py:24)
       ProfScope ps(m, EVT_PROF_QKV, s);
       DenseCall c;
       c.flags = EPI_LNIN | EPI_BIAS;
       c.A = m->x; c.lda = D; c.C = m->qkv; c.ldc = 3 * L.inner; c.M = rows; c.N = 3 * L.inner;
       c.stats_in = m->sx;
+      if (L.hd == 64 && m->headmajor) {
+        DenseCall h = c;
+        h.flags |= EPI_HM;
+        h.ldc = 64;
+        h.P = T;
+        if (gemm_headmajor_ok(m->dtype, h.flags, dense_params(m, L.qkv, h))) {
+          c = h;
+          hm = true;
+        }
+      }
       EVT_RC(dense(m, L.qkv, c, s));
     }
     {
@@ -537,6 +561,13 @@ int run_encoder(evt_model* m, int B, hipStream_t s) {
                 (double)rows * 4 * L.inner * elem_size(m->dtype));  // qkv read + O written
       AttnParams ap{m->qkv, 3 * L.inner, m->o, L.inner, T, L.heads, B, scale_log2};
       ap.hd = L.hd;
+      if (hm) {
+        ap.ldq = 64;
+        ap.sb = (int64_t)L.heads * 3 * T * 64;
+        ap.sh = (int64_t)3 * T * 64;
+        ap.ko = T * 64;
+        ap.vo = 2 * T * 64;
+      }
       EVT_HIP(attention_launch(m->dtype, ap, s), "attention");
     }
     // out-proj + bias + LN1(x) residual -> xm (+ stats); STANDARD: + x

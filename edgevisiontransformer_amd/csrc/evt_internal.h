@@ -22,6 +22,9 @@ enum : int {
   EPI_OUT_MX8 = 512,   // MXFP8 output (mx8.hip GEMM only)
   EPI_GATHER = 1024,   // A rows gathered by the GEMM's loader: Swin PatchMerging (GemmParams g*)
   EPI_SPLIT = 2048,    // A rows gathered by the GEMM's loader: T2T soft split k3 s2 p1 (g*)
+  EPI_HM = 4096,       // head-major QKV output [B][H][q | k | v][P][64] (P = tokens per image,
+                       // N = 3 H 64): q, k, v of every (image, head) contiguous runs for the
+                       // attention kernel (AttnParams sb / sh / ko / vo). Persistent kernel only
 };
 
 // C[M, N] = epilogue(A[M, K] . W[K, N]) with W pre-packed K-contiguous as Wp[Npad][Kpad].
@@ -70,6 +73,9 @@ hipError_t gemm_launch(int dtype, int flags, const GemmParams& p, hipStream_t s)
 // part[S][M][ntiles*128], then a fixed-order reduction + bias (+ GELU) into C (deterministic).
 // flags: EPI_BIAS and/or EPI_GELU and/or EPI_OUT_F32 only; K % (S * 64) == 0.
 int device_cus();  // compute units of the current device (cached)
+// whether gemm_launch(dtype, flags | EPI_HM, p) runs (the persistent 256 x 256 kernel with its
+// head-major store; N = 3 H 64, M N 2 < 2^31); the caller keeps the token-major layout otherwise
+bool gemm_headmajor_ok(int dtype, int flags, const GemmParams& p);
 hipError_t gemm_splitk_launch(int dtype, int flags, const GemmParams& p, int S, float* part,
                               hipStream_t s);
 void gemm_set_variant(int v);
@@ -99,6 +105,13 @@ struct AttnParams {
   int64_t ldq8 = 0;
   int rows8 = 0;
   int hd = 64;                    // head size h_k (<= 128; 64: the tuned kernels, else generic)
+  // qkv addressing of the bf16 h_k = 64 kernels: (image b, head h) slice at qkv + b sb + h sh
+  // (elements), its rows ldq apart, q / k / v at columns 0 / ko / vo of a row. All zero = the
+  // token-major layout above (sb = N ldq, sh = 64, ko = H 64, vo = 2 H 64); the head-major layout
+  // of the model's QKV GEMM (EPI_HM: [B][H][q | k | v][N][64]) sets sb = 3 H N 64, sh = 3 N 64,
+  // ldq = 64, ko = N 64, vo = 2 N 64 (q, k and v of a slice each one contiguous run)
+  int64_t sb = 0, sh = 0;
+  int ko = 0, vo = 0;
 };
 hipError_t attention_launch(int dtype, const AttnParams& p, hipStream_t s);
 

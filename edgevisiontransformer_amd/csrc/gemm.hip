@@ -1531,7 +1531,22 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
     const bool rcol_ok = !PADN || interior || n0 + wn * 64 + rch * 8 < p.N;
     __amdgpu_buffer_rsrc_t cs;
     int vo = ((wm * 128 + rrow) * (int)p.ldc + wn * 64 + rch * 8) * 2, orow0 = 0;
-    if constexpr ((FL & EPI_POS) != 0) {  // output rows b*(P+1) + 1 + t, base at tile row 0
+    // EPI_HM: this wave's 64 columns are one (part, head) of q | k | v; row m = (b, t) goes to
+    // (((b H + h) 3 + part) P + t) 64 + ... of the whole buffer (rows past M land past its end)
+    // (lane row base = m0 + wm 128 + rrow as image b0, token t0; the stored rows are base + 8 j,
+    // j < 16, at most one image boundary past it for P >= 128, else pos_img per row)
+    int hm_b0 = 0, hm_t0 = 0, hm_col = 0, hm_HP = 0;
+    if constexpr ((FL & EPI_HM) != 0) {
+      const int inner = p.N / 3, c0 = n0 + wn * 64;
+      const int part = __builtin_amdgcn_readfirstlane(c0 / inner);
+      const int h = __builtin_amdgcn_readfirstlane((c0 - part * inner) >> 6);
+      hm_HP = 3 * (inner >> 6) * p.P;                      // rows of one image's slices
+      hm_col = ((3 * h + part) * p.P * 64 + rch * 8) * 2;  // + ((b 3 H P + t) 64) 2
+      const int base = m0 + wm * 128 + rrow;
+      hm_b0 = pos_img(base, p.P);
+      hm_t0 = base - hm_b0 * p.P;
+      cs = __builtin_amdgcn_make_buffer_rsrc(p.C, 0, p.M * p.N * 2, 0x00020000);
+    } else if constexpr ((FL & EPI_POS) != 0) {  // output rows b*(P+1) + 1 + t, base at tile row 0
       orow0 = __builtin_amdgcn_readfirstlane(pos_orow(m0, p.P));
       const int olast = pos_orow(min(m0 + BIG_BM, p.M) - 1, p.P);
       const int nr = ((olast + 1 - orow0) * (int)p.ldc - n0) * 2;
@@ -1557,7 +1572,20 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
           keep = (v[0] ^ v[1] ^ v[2] ^ v[3]) == 0x12345u;
         }
         int so = __builtin_amdgcn_readfirstlane((32 * k + 8 * i) * (int)p.ldc * 2), svo = vo;
-        if constexpr ((FL & EPI_POS) != 0) {  // per-lane remapped row (rows past M: beyond nr)
+        if constexpr ((FL & EPI_HM) != 0) {  // per-lane head-major row
+          int b = hm_b0, t = hm_t0 + 32 * k + 8 * i;
+          if (p.P >= 128) {
+            const bool wrap = t >= p.P;
+            b += wrap ? 1 : 0;
+            t -= wrap ? p.P : 0;
+          } else {
+            const int m = m0 + wm * 128 + 32 * k + 8 * i + rrow;
+            b = pos_img(m, p.P);
+            t = m - b * p.P;
+          }
+          so = 0;
+          svo = (b * hm_HP + t) * 128 + hm_col;
+        } else if constexpr ((FL & EPI_POS) != 0) {  // per-lane remapped row (rows past M: beyond nr)
           so = 0;
           svo = ((pos_orow(m0 + wm * 128 + 32 * k + 8 * i + rrow, p.P) - orow0) * (int)p.ldc +
                  wn * 64 + rch * 8) * 2;
@@ -2302,7 +2330,8 @@ constexpr bool pers_fl(int fl) {
          fl == (EPI_LNIN | EPI_BIAS | EPI_GELU_ERF) || fl == (EPI_BIAS | EPI_RESID | EPI_STATS) ||
          fl == (EPI_LNIN | EPI_BIAS | EPI_STATS) ||
          fl == (EPI_LNIN | EPI_BIAS | EPI_STATS | EPI_GATHER) ||
-         fl == (EPI_LNIN | EPI_BIAS | EPI_SPLIT) || fl == (EPI_BIAS | EPI_POS | EPI_STATS | EPI_SPLIT);
+         fl == (EPI_LNIN | EPI_BIAS | EPI_SPLIT) || fl == (EPI_BIAS | EPI_POS | EPI_STATS | EPI_SPLIT) ||
+         fl == (EPI_LNIN | EPI_BIAS | EPI_HM);
 }
 
 // persistent kernel: supported epilogue, 8-column output groups, LN rows of <= 8 slots
@@ -2441,9 +2470,19 @@ hipError_t launch_sk(const GemmParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+bool headmajor_fits(const GemmParams& p) {
+  return p.N % 192 == 0 && p.P > 0 && p.M % p.P == 0 && p.M < (1 << 22) &&
+         (int64_t)p.M * p.N * 2 < ((int64_t)1 << 31) && g_gemm_variant != 16 && g_gemm_variant != 30;
+}
+
 template <typename T, int FL>
 hipError_t launch_t(const GemmParams& p, hipStream_t s) {
-  if constexpr ((FL & (EPI_GATHER | EPI_SPLIT)) != 0) {  // gathering loader: persistent kernel
+  if constexpr ((FL & EPI_HM) != 0) {  // head-major store: the persistent kernel or nothing
+    if constexpr (std::is_same<T, bf16>::value && pers_fl(FL)) {
+      if (headmajor_fits(p) && use_big(p, FL) && use_pers(p, FL)) return launch_pers<FL>(p, s);
+    }
+    return hipErrorNotSupported;
+  } else if constexpr ((FL & (EPI_GATHER | EPI_SPLIT)) != 0) {  // gathering loader: persistent kernel
     if constexpr (std::is_same<T, bf16>::value) {
       constexpr bool MERGE = (FL & EPI_GATHER) != 0;
       const bool merge = MERGE && p.gmode == 1 && p.gR % 2 == 0 && p.gOW == p.gR / 2 &&
@@ -2496,6 +2535,7 @@ hipError_t dispatch(int flags, const GemmParams& p, hipStream_t s) {
     EVT_CASE(EPI_BIAS | EPI_POS | EPI_STATS | EPI_SPLIT)     // T2T soft_split2 + project
     EVT_CASE(EPI_BIAS | EPI_RESID | EPI_STATS)               // Swin proj / FC2 + plain residual
     EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_STATS)                // Swin LN-folded patch-merge reduction
+    EVT_CASE(EPI_LNIN | EPI_BIAS | EPI_HM)                   // LN1-folded QKV, head-major output
 #undef EVT_CASE
     default: return hipErrorInvalidValue;
   }
@@ -2615,6 +2655,12 @@ size_t gemm_sk_bytes() { return 4096 + (size_t)SK_MAX_G * SK_SLOT_FLOATS * sizeo
 void gemm_sk_bind(void* ws, GemmParams& p) {
   p.sk_flags = ws ? (int*)ws : nullptr;
   p.sk_part = ws ? (float*)((char*)ws + 4096) : nullptr;
+}
+
+bool gemm_headmajor_ok(int dtype, int flags, const GemmParams& p) {
+  constexpr int F = EPI_LNIN | EPI_BIAS | EPI_HM;
+  return dtype == DT_BF16 && (flags | EPI_HM) == F && p.K % PAD_K == 0 && p.K > 0 &&
+         p.ntiles * GEMM_BN >= p.N && headmajor_fits(p) && use_big(p, F) && use_pers(p, F);
 }
 
 hipError_t gemm_launch(int dtype, int flags, const GemmParams& p, hipStream_t s) {

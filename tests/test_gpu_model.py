@@ -90,6 +90,33 @@ def test_batch_independence(gpu, dtype):
     assert torch.equal(torch.roll(auto, 11, 0), rolled)
 
 
+@pytest.mark.parametrize("which,batch", [("deit_tiny", 64), ("deit_base", 20), ("pruned", 48),
+                                         ("deit_tiny", 3)])
+def test_qkv_head_major_bitwise(gpu, monkeypatch, which, batch):
+    """The head-major qkv layout (the QKV GEMM's EPI_HM store + the attention's slice strides; used
+    where that GEMM runs the persistent kernel: every case here but the 3-image one) against the
+    token-major layout (EVT_QKV_LAYOUT=token at model creation): the same arithmetic at other
+    addresses, so the logits agree bit for bit. 'pruned': per-layer head counts 1-3 (QKV widths
+    192-576, column-padded tiles)."""
+    from edgevisiontransformer_amd.modeling.models import vit
+
+    def build():
+        if which == "pruned":
+            return ViT_Pruned(dim=192, depth=6, heads=3, mlp_dim=768, head_size=64,
+                              prune_encoding="layerwise_h1-d0.5_h3-d1.0_h2-d0.3_h3-d0.7_h1-d1.0_h2-d0.2",
+                              dtype="bf16", seed=12, device=gpu)
+        return getattr(vit, f"get_{which}")(dtype="bf16", seed=12, device=gpu)
+
+    img = torch.from_numpy(make_images(batch, seed=21)).to(gpu)
+    monkeypatch.setenv("EVT_QKV_LAYOUT", "token")
+    tok = build()(img)
+    monkeypatch.delenv("EVT_QKV_LAYOUT")
+    hm = build()(img)
+    torch.cuda.synchronize()
+    assert torch.isfinite(hm).all()
+    assert torch.equal(tok, hm)
+
+
 def test_deit_small_bf16_vs_oracle(gpu):
     from edgevisiontransformer_amd.modeling.models.vit import get_deit_small
     m = get_deit_small(dtype="bf16", seed=4, device=gpu)
