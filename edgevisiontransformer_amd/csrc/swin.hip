@@ -912,15 +912,6 @@ __global__ __launch_bounds__(256, 2) void swin_attn96_kernel(SwinAttnBlockParams
     // region mask and the keys past 48 as -inf); the next window's x prefetch lands during P2 / P3
     const int qt = wave;
     if (wg + (int)gridDim.x < nwin) prefetch(wg + gridDim.x);
-#ifdef EVT_AT96_XRPF
-    // P3's residual rows (L2-resident: read by this window's prefetch), loaded before the heads
-    bf16x4 xr[6];
-    {
-      const int64_t row = G.row(min(16 * qt + c16, 48));
-#pragma unroll
-      for (int f = 0; f < 6; ++f) xr[f] = *(const bf16x4*)(x + row * 96 + 16 * f + 4 * g);
-    }
-#endif
     const int wtype = G.type();
     const bool lr_ = wtype & 2, lc_ = wtype & 1;
     const int qq = min(16 * qt + c16, 48), qi = (qq * 37) >> 8, qj = qq - 7 * qi;
@@ -1008,11 +999,9 @@ __global__ __launch_bounds__(256, 2) void swin_attn96_kernel(SwinAttnBlockParams
     {
       const int t = 16 * qt + c16;
       const int64_t row = G.row(min(t, 48));
-#ifndef EVT_AT96_XRPF
       bf16x4 xr[6];  // residual rows (L2-resident: read by this window's prefetch)
 #pragma unroll
       for (int f = 0; f < 6; ++f) xr[f] = *(const bf16x4*)(x + row * 96 + 16 * f + 4 * g);
-#endif
       u32x4 bo[3];
 #pragma unroll
       for (int ks = 0; ks < 3; ++ks)
