@@ -19,7 +19,8 @@ import sys
 # demangles the float instantiations but not the bf16 (DF16b) ones of gemm_nt_kernel
 RULES = {
     ("vit", "bf16"): {"fc1": [("gemm_pers_kernel<35,", 1, 0)],
-                      "qkv": [("gemm_pers_kernel<33,", 1, 0)],
+                      # (4129 = LNIN | BIAS | HM: the head-major qkv store, round 5)
+                      "qkv": [("gemm_pers_kernel<33,", 1, 0), ("gemm_pers_kernel<4129,", 1, 0)],
                       "out_proj": [("gemm_pers_kernel<197,", 2, 0), ("gemm_nt_kernelIDF16bLi197E", 2, 0)],
                       "fc2": [("gemm_pers_kernel<197,", 2, 1), ("gemm_nt_kernelIDF16bLi197E", 2, 1)],
                       "attention": [("attn_bf16_kernel", 1, 0)]},
