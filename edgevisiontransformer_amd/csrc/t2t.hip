@@ -278,13 +278,42 @@ __global__ __launch_bounds__(256) void performer_kv_kernel(const T* __restrict__
     for (int mt = 0; mt < 2; ++mt) acc[nt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float ks[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // ksum partial, m = 16mt + 4(l>>4) + j
   const int tr = lane & 15, g4 = 4 * (lane >> 4);
+  // PERM (the model's bf16 path): the next tile's raw k / v pieces are loaded while this one runs
+  // (round 5: the loads were issued and consumed in the same iteration, 65 % of the wave cycles in
+  // s_waitcnt); a row past the chunk loads the chunk's first row and is zeroed on use
+  u32x4 rk[2], rv[2];
+  auto raw = [&](int t0n) {
+    const int tn = t0n + tr;
+    const T* rowp = kqv + ((int64_t)b * ntok + (tn < t_hi ? tn : t_lo)) * ldq + 16 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      rk[i] = *(const u32x4*)(rowp + 8 * i);
+      rv[i] = *(const u32x4*)(rowp + 2 * PF_HS + 8 * i);
+    }
+  };
+  if constexpr (PERM) {
+    if (t_lo + 16 * wave < t_hi) raw(t_lo + 16 * wave);
+  }
   for (int t0 = t_lo + 16 * wave; t0 < t_hi; t0 += 64) {
     const int t = t0 + tr;
     const bool valid = t < t_hi;
     const T* rowp = kqv + ((int64_t)b * ntok + t) * ldq;
     f32x4 kf[4], vf[4];
-    load_block<T, PERM>(rowp, valid, lane, kf);              // k = columns [0, 64) (split order k, q, v)
-    load_block<T, PERM>(rowp + 2 * PF_HS, valid, lane, vf);  // v = columns [128, 192)
+    if constexpr (PERM) {  // the same fragments as load_block<T, true>
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const bf16x8 kv8 = __builtin_bit_cast(bf16x8, rk[c >> 1]), vv8 = __builtin_bit_cast(bf16x8, rv[c >> 1]);
+        const int o = 4 * (c & 1);
+        kf[c] = valid ? f32x4{(float)kv8[o], (float)kv8[o + 1], (float)kv8[o + 2], (float)kv8[o + 3]}
+                      : f32x4{0.f, 0.f, 0.f, 0.f};
+        vf[c] = valid ? f32x4{(float)vv8[o], (float)vv8[o + 1], (float)vv8[o + 2], (float)vv8[o + 3]}
+                      : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      if (t0 + 64 < t_hi) raw(t0 + 64);
+    } else {
+      load_block<T, PERM>(rowp, valid, lane, kf);              // k = columns [0, 64) (split order k, q, v)
+      load_block<T, PERM>(rowp + 2 * PF_HS, valid, lane, vf);  // v = columns [128, 192)
+    }
     float kd = 0.f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) kd += kf[c][0] * kf[c][0] + kf[c][1] * kf[c][1] + kf[c][2] * kf[c][2] + kf[c][3] * kf[c][3];
