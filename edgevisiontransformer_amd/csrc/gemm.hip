@@ -1535,7 +1535,7 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
     // (((b H + h) 3 + part) P + t) 64 + ... of the whole buffer (rows past M land past its end)
     // (lane row base = m0 + wm 128 + rrow as image b0, token t0; the stored rows are base + 8 j,
     // j < 16, at most one image boundary past it for P >= 128, else pos_img per row)
-    int hm_b0 = 0, hm_t0 = 0, hm_col = 0, hm_HP = 0;
+    int hm_b0 = 0, hm_t0 = 0, hm_col = 0, hm_HP = 0, hm_r0 = 0, hm_wrap = 0;
     if constexpr ((FL & EPI_HM) != 0) {
       const int inner = p.N / 3, c0 = n0 + wn * 64;
       const int part = __builtin_amdgcn_readfirstlane(c0 / inner);
@@ -1545,6 +1545,8 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
       const int base = m0 + wm * 128 + rrow;
       hm_b0 = pos_img(base, p.P);
       hm_t0 = base - hm_b0 * p.P;
+      hm_r0 = (hm_b0 * hm_HP + hm_t0) * 128 + hm_col;  // the lane's first row; + 8 j rows: + 1 KiB j
+      hm_wrap = (hm_HP - p.P) * 128;                   // past the image's last token: the next image
       cs = __builtin_amdgcn_make_buffer_rsrc(p.C, 0, p.M * p.N * 2, 0x00020000);
     } else if constexpr ((FL & EPI_POS) != 0) {  // output rows b*(P+1) + 1 + t, base at tile row 0
       orow0 = __builtin_amdgcn_readfirstlane(pos_orow(m0, p.P));
@@ -1573,18 +1575,15 @@ __device__ __forceinline__ void pers_epilogue(const GemmParams& p, char* smem, f
         }
         int so = __builtin_amdgcn_readfirstlane((32 * k + 8 * i) * (int)p.ldc * 2), svo = vo;
         if constexpr ((FL & EPI_HM) != 0) {  // per-lane head-major row
-          int b = hm_b0, t = hm_t0 + 32 * k + 8 * i;
-          if (p.P >= 128) {
-            const bool wrap = t >= p.P;
-            b += wrap ? 1 : 0;
-            t -= wrap ? p.P : 0;
+          if (p.P >= 128) {  // row offset 8 j (< P): one compare / select per store, j in soffset
+            so = __builtin_amdgcn_readfirstlane((32 * k + 8 * i) * 128);
+            svo = hm_r0 + (hm_t0 + 32 * k + 8 * i >= p.P ? hm_wrap : 0);
           } else {
             const int m = m0 + wm * 128 + 32 * k + 8 * i + rrow;
-            b = pos_img(m, p.P);
-            t = m - b * p.P;
+            const int b = pos_img(m, p.P), t = m - b * p.P;
+            so = 0;
+            svo = (b * hm_HP + t) * 128 + hm_col;
           }
-          so = 0;
-          svo = (b * hm_HP + t) * 128 + hm_col;
         } else if constexpr ((FL & EPI_POS) != 0) {  // per-lane remapped row (rows past M: beyond nr)
           so = 0;
           svo = ((pos_orow(m0 + wm * 128 + 32 * k + 8 * i + rrow, p.P) - orow0) * (int)p.ldc +
