@@ -30,6 +30,7 @@ RULES = {
                      "fc2": [("gemm_nt_kernel<float, 197>", 2, 1)],
                      "attention": [("attn_f32_kernel", 1, 0)]},
     ("t2t", "bf16"): {"fc1": [("gemm_pers_kernel<35,", 1, 0)],
+                      "qkv": [("gemm_pers_kernel<4129,", 1, 0)],  # head-major store (the kqv GEMMs are <33>)
                       "out_proj": [("gemm_pers_kernel<197,", 2, 0)],
                       "fc2": [("gemm_pers_kernel<197,", 2, 1)],
                       "attention": [("attn_bf16_kernel", 1, 0)]},
