@@ -597,25 +597,6 @@ constexpr int MLP96_LDS = MLP96_F * MLP96_W1_ROW + MLP96_C * MLP96_W2_ROW;  // 1
 // SIMD idle on latencies that a third wave fills
 constexpr int MLP96_WAVES = 12;
 
-#ifdef EVT_MLP_STAMPS
-// lab diagnostic: s_memtime stamps of the first 4 tiles of every wave (wave-uniform, lane 0 stores)
-__device__ unsigned long long evt_mlp_stamps[1024 * 16 * 4 * 16];
-#define MLP_STAMP(k)                                                                             \
-  do {                                                                                           \
-    if (it_ < 4 && lane == 0)                                                                    \
-      evt_mlp_stamps[(((int64_t)blockIdx.x * MLP96_WAVES + wave) * 4 + it_) * 16 + (k)] =        \
-          __builtin_amdgcn_s_memtime();                                                          \
-  } while (0)
-#define MLP_RSTAMP(k)                                                                            \
-  do {                                                                                           \
-    if (it_ < 4 && lane == 0)                                                                    \
-      evt_mlp_stamps[(((int64_t)blockIdx.x * MLP96_WAVES + wave) * 4 + it_) * 16 + (k)] =        \
-          __builtin_amdgcn_s_memrealtime();                                                      \
-  } while (0)
-#else
-#define MLP_STAMP(k) do {} while (0)
-#define MLP_RSTAMP(k) do {} while (0)
-#endif
 
 __global__ __launch_bounds__(64 * MLP96_WAVES, 1) void swin_mlp96_kernel(SwinMlpParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -640,11 +621,7 @@ __global__ __launch_bounds__(64 * MLP96_WAVES, 1) void swin_mlp96_kernel(SwinMlp
   __syncthreads();
   const float inv_d = 1.0f / (float)MLP96_C;
   const int ntiles = (p.M + 31) / 32;
-  int it_ = 0;
-  (void)it_;
-  for (int t = blockIdx.x * MLP96_WAVES + wave; t < ntiles; t += gridDim.x * MLP96_WAVES, ++it_) {
-    MLP_STAMP(0);
-    MLP_RSTAMP(10);
+  for (int t = blockIdx.x * MLP96_WAVES + wave; t < ntiles; t += gridDim.x * MLP96_WAVES) {
     const int tok0 = t * 32;
     // B operand of FC1: LN2(xm) of token (16 tt + c16), k 32 ks + 8 g .. + 7, normalised in
     // registers ((x - mu) r; gamma is folded into W1, beta.W1 + b1 = cvec seeds the accumulator)
@@ -679,7 +656,6 @@ __global__ __launch_bounds__(64 * MLP96_WAVES, 1) void swin_mlp96_kernel(SwinMlp
     f32x4 out[6][2];
 #pragma unroll
     for (int ct = 0; ct < 6; ++ct) out[ct][0] = out[ct][1] = load4(p.b2 + ct * 16 + 4 * g);
-    MLP_STAMP(1);
 #pragma unroll 2
     for (int hc = 0; hc < 12; ++hc) {
       f32x4 h[2][2];
@@ -696,7 +672,6 @@ __global__ __launch_bounds__(64 * MLP96_WAVES, 1) void swin_mlp96_kernel(SwinMlp
                 __builtin_bit_cast(bf16x8, wv), __builtin_bit_cast(bf16x8, a[tt][ks]), h[ht][tt], 0, 0, 0);
         }
       }
-      if (hc < 2) MLP_STAMP(2 + 3 * hc);
       // h[ht][tt][jj]: hidden 32 hc + 16 ht + 4 g + jj, token 16 tt + c16 (bias included) -> GELU,
       // packed straight into the FC2 B operand (k slots 8 g .. 8 g + 7 = [ht 0 jj 0..3 | ht 1])
       u32x4 pf[2];
@@ -709,7 +684,6 @@ __global__ __launch_bounds__(64 * MLP96_WAVES, 1) void swin_mlp96_kernel(SwinMlp
           pf[tt][2 * ht] = __builtin_bit_cast(unsigned, __builtin_convertvector(lo, bf16x2));
           pf[tt][2 * ht + 1] = __builtin_bit_cast(unsigned, __builtin_convertvector(hi, bf16x2));
         }
-      if (hc < 2) MLP_STAMP(3 + 3 * hc);
 #pragma unroll
       for (int ct = 0; ct < 6; ++ct) {
         const u32x4 wv = *(const EVT_LDS u32x4*)(W2s + (ct * 16 + c16) * MLP96_W2_ROW + hc * 64 + 16 * g);
@@ -718,9 +692,7 @@ __global__ __launch_bounds__(64 * MLP96_WAVES, 1) void swin_mlp96_kernel(SwinMlp
           out[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
               __builtin_bit_cast(bf16x8, wv), __builtin_bit_cast(bf16x8, pf[tt]), out[ct][tt], 0, 0, 0);
       }
-      if (hc < 2) MLP_STAMP(4 + 3 * hc);
     }
-    MLP_STAMP(8);
     // out[ct][tt][jj]: feature 16 ct + 4 g + jj, token 16 tt + c16: + b2 + xm, store x, stats
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt) {
@@ -752,8 +724,6 @@ __global__ __launch_bounds__(64 * MLP96_WAVES, 1) void swin_mlp96_kernel(SwinMlp
         so[1] = g == 0 ? s2 : 0.f;
       }
     }
-    MLP_STAMP(9);
-    MLP_RSTAMP(11);
   }
 }
 
@@ -1298,15 +1268,6 @@ hipError_t window_attn_launch(int dtype, const SwinAttnParams& p, hipStream_t s)
   return hipGetLastError();
 }
 
-#ifdef EVT_MLP_STAMPS
-}  // namespace evt
-extern "C" int evt_lab_mlp_stamps(void* dst, size_t bytes) {
-  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(evt::evt_mlp_stamps),
-                                  std::min(bytes, sizeof(evt::evt_mlp_stamps)), 0,
-                                  hipMemcpyDeviceToHost);
-}
-namespace evt {
-#endif
 hipError_t swin_mlp96_launch(const SwinMlpParams& p, hipStream_t s) {
   if (p.M <= 0) return hipSuccess;
   if (p.nslots < 1 || p.nslots > 4 || p.ldw1 < MLP96_C || p.ldw2 < MLP96_F || p.ldw1 % 8 ||
