@@ -597,7 +597,6 @@ constexpr int MLP96_LDS = MLP96_F * MLP96_W1_ROW + MLP96_C * MLP96_W2_ROW;  // 1
 // SIMD idle on latencies that a third wave fills
 constexpr int MLP96_WAVES = 12;
 
-
 __global__ __launch_bounds__(64 * MLP96_WAVES, 1) void swin_mlp96_kernel(SwinMlpParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   EVT_LDS char* W1s = (EVT_LDS char*)smem;
