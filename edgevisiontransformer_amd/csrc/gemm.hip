@@ -808,6 +808,124 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem,
   }
 }
 
+// Two-phase schedule (big8_loop<..., KT2 = true>: the LN-folded FC1 + GELU kernels only): per
+// K-tile and wave group two MFMA bursts of 32 (n-halves 0 and 1 of m-half 0, then of m-half 1)
+// instead of four of 16 (FC1 -1.5 %; the instances with residual or head-major epilogues spill
+// with it, profiles/r05_gemm_two_phase_ab.txt). The region stream keeps the order of
+// big8_prologue; regions 0..2 of K-tile T are issued in phase 1 of K-tile T - 2, region 3 in phase
+// 0 of K-tile T - 1 (one K-tile of flight each), 8 glds per lane younger at every wait; K-tile 1's
+// region 2 waits for K-tile 0's phase 0 (the epilogue's scratch is in it: with cont, the previous
+// tile's last K-tile issues the next tile's (0, 0..3), (1, 0..1) like big8_prologue). WAR: a
+// region is overwritten one barrier after its last read, so every wave retires its fragment reads
+// (lgkmcnt 0) before its opening barrier.
+template <int MODE, int X, bool OPEN = false, int X3 = 0, typename Ph3 = NoOp,
+          typename P = GemmParams>
+__device__ __forceinline__ void big8_ktile2(const P& p, char* smem,
+                                            f32x4 (&acc)[GeoOf<P>::NF][GeoOf<P>::MF],
+                                            int wave, int lane, int wm, int wn, int m0, int n0,
+                                            int t, bool cont = false, int nm0 = 0, int nn0 = 0,
+                                            Ph3 ph3 = {}, int par = 0, int npar = 0) {
+  typedef Geo<P> Gm;
+  constexpr int MH = Gm::MH, NH = Gm::NH;
+  // phase 0 reads regions 0..2 (and, 128 x 384, the first instruction of region 3): 8 younger
+  // glds after region 2, 7 after that instruction (big8_stage's paired order)
+  constexpr int W0 = Gm::WI == 3 ? 7 : 8;
+  const int frow = lane & 15, fsw = lane & 7, fg = lane >> 4;
+  const EVT_LDS char* As = (const EVT_LDS char*)smem + ((t ^ par) & 1) * BIG_STAGE;
+  const EVT_LDS char* Ws = As + Gm::A_TILE;
+  auto rd = [&](const EVT_LDS char* S, int row, int ks) {
+    return *(const EVT_LDS u32x4*)(S + row * ROWB + (((fg + 4 * ks) ^ fsw) << 4));
+  };
+  u32x4 af[MH][2], bf0[NH][2], bf1[NH][2];
+#pragma unroll
+  for (int ph = 0; ph < 2; ++ph) {
+    // the DMA first: its address arithmetic then overlaps dead fragment registers (issued after
+    // the reads it spilled in the out-proj / QKV instantiations)
+    if (MODE == 0 || (MODE == 1 && ph == 0)) {
+      if (ph == 0) {
+        if (t == 0) big8_stage(p, smem, wave, lane, m0, n0, 1, 2, par);
+        big8_stage(p, smem, wave, lane, m0, n0, t + 1, 3, par);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) big8_stage(p, smem, wave, lane, m0, n0, t + 2, j, par);
+      }
+    } else if (cont) {  // the next tile's regions: (0, 0..2) | (0, 3), (1, 0..1)
+      if (ph == 0) {
+        big8_stage(p, smem, wave, lane, nm0, nn0, 0, 3, npar);
+      } else {
+#pragma unroll
+        for (int j = 0; j < (MODE == 1 ? 3 : 2); ++j)
+          big8_stage(p, smem, wave, lane, nm0, nn0, MODE == 1 ? 0 : 1, j, npar);
+      }
+    }
+    if (ph == 0) {
+#pragma unroll
+      for (int nt = 0; nt < NH; ++nt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) bf0[nt][ks] = rd(Ws, wn * Gm::WC + nt * 16 + frow, ks);
+#pragma unroll
+      for (int mt = 0; mt < MH; ++mt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) af[mt][ks] = rd(As, wm * Gm::WR + mt * 16 + frow, ks);
+#pragma unroll
+      for (int nt = 0; nt < NH; ++nt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          bf1[nt][ks] = rd(Ws, wn * Gm::WC + Gm::WC / 2 + nt * 16 + frow, ks);
+    } else {
+#pragma unroll
+      for (int mt = 0; mt < MH; ++mt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          af[mt][ks] = rd(As, wm * Gm::WR + Gm::WR / 2 + mt * 16 + frow, ks);
+    }
+    // retire what the next phase reads: region 3 after phase 0 (X: younger, issued before the
+    // K-tile), the next K-tile's regions 0..2 after phase 1 (X older than those)
+    if (ph == 0) {
+      if (MODE != 2 || cont) wait_vm<8 + X>();
+      else wait_vm<0 + X>();
+    } else if (MODE == 0 || (MODE == 1 && cont)) {
+      wait_vm<W0>();
+    } else if (MODE == 1) {
+      wait_vm<W0 - 6>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    big8_bar();
+    __builtin_amdgcn_sched_barrier(0);
+    const int mb = ph ? MH : 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int nb = (ph ^ h) ? NH : 0;  // phase 0: n-half 0 then 1; phase 1: 1 then 0
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int nt = 0; nt < NH; ++nt)
+#pragma unroll
+          for (int mt = 0; mt < MH; ++mt)
+            Mma<bf16>::run(nb ? bf1[nt][ks] : bf0[nt][ks], af[mt][ks], acc[nb + nt][mb + mt]);
+      // the X3 loads once the n-half-1 fragments are dead (their registers)
+      if (ph == 1 && h == 0) ph3();
+    }
+    if (!(OPEN && MODE == 2 && ph == 1 && wm == 1)) big8_bar();
+  }
+}
+
+// one K-tile of either schedule
+template <bool KT2, int MODE, int X, bool OPEN = false, int X3 = 0, typename Ph3 = NoOp,
+          typename P = GemmParams>
+__device__ __forceinline__ void big8_kt(const P& p, char* smem,
+                                        f32x4 (&acc)[GeoOf<P>::NF][GeoOf<P>::MF], int wave,
+                                        int lane, int wm, int wn, int m0, int n0, int t,
+                                        bool cont = false, int nm0 = 0, int nn0 = 0, Ph3 ph3 = {},
+                                        int par = 0, int npar = 0) {
+  if constexpr (KT2)
+    big8_ktile2<MODE, X, OPEN, X3>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, cont, nm0, nn0,
+                                   ph3, par, npar);
+  else
+    big8_ktile<MODE, X, OPEN, X3>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, cont, nm0, nn0,
+                                  ph3, par, npar);
+}
+
 // Main loop over the nk K-tiles after big8_prologue (whose DMAs may be followed by X further
 // VMEM instructions per wave, or by a vmcnt(0)). Ends with every wave past a common barrier.
 // pre1: run by wave group 1 in the slot where it waits one barrier for group 0 (per-tile LDS
@@ -816,7 +934,8 @@ __device__ __forceinline__ void big8_ktile(const P& p, char* smem,
 // they are younger than every DMA that tile waits for); last3: LX3 more at the start of the last
 // K-tile's phase 3.
 template <int X, bool OPEN = false, typename Pre1 = NoOp, typename Mid = NoOp, int LX = 0,
-          typename Last = NoOp, int LX3 = 0, typename Last3 = NoOp, typename P = GemmParams>
+          typename Last = NoOp, int LX3 = 0, typename Last3 = NoOp, typename P = GemmParams,
+          bool KT2 = false>
 __device__ __forceinline__ void big8_loop(const P& p, char* smem,
                                           f32x4 (&acc)[GeoOf<P>::NF][GeoOf<P>::MF],
                                           int wave, int lane, int wm, int wn, int m0, int n0,
@@ -826,31 +945,38 @@ __device__ __forceinline__ void big8_loop(const P& p, char* smem,
   // K-tile t of this tile sits in buffer (t ^ par) & 1; the next tile (cont) starts at the parity
   // of stream K-tile nk
   const int npar = par ^ (nk & 1);
-  if (nk >= 2) wait_vm<8 + X>();
-  else wait_vm<4 + X>();
+  if constexpr (KT2) {
+    // phase 0 reads regions 0..2 (big8_ktile2): younger are (0, 3) and (1, 0..1)
+    constexpr int W0 = Geo<P>::WI == 3 ? 7 : 8;
+    if (nk >= 2) wait_vm<W0 - 2 + X>();
+    else wait_vm<W0 - 6 + X>();
+  } else {
+    if (nk >= 2) wait_vm<8 + X>();
+    else wait_vm<4 + X>();
+  }
   big8_bar();
   if (wm == 1) {
     pre1();
     big8_bar();
   }
   if (nk >= 3) {
-    big8_ktile<0, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, false, 0, 0, {}, par, 0);
+    big8_kt<KT2, 0, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, false, 0, 0, {}, par, 0);
     mid();
     int t = 1;
     for (; t + 2 < nk; ++t)
-      big8_ktile<0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, false, 0, 0, {}, par, 0);
-    big8_ktile<1, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, cont, nm0, nn0, {}, par, npar);
+      big8_kt<KT2, 0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, false, 0, 0, {}, par, 0);
+    big8_kt<KT2, 1, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, cont, nm0, nn0, {}, par, npar);
     last();
-    big8_ktile<2, LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1, cont, nm0, nn0,
+    big8_kt<KT2, 2, LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1, cont, nm0, nn0,
                                  last3, par, npar);
   } else if (nk == 2) {
-    big8_ktile<1, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, cont, nm0, nn0, {}, par, npar);
+    big8_kt<KT2, 1, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, cont, nm0, nn0, {}, par, npar);
     last();
-    big8_ktile<2, LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, 1, cont, nm0, nn0, last3,
+    big8_kt<KT2, 2, LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, 1, cont, nm0, nn0, last3,
                                  par, npar);
   } else {
     last();
-    big8_ktile<2, X + LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, false, 0, 0,
+    big8_kt<KT2, 2, X + LX, OPEN, LX3>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, false, 0, 0,
                                      last3, par);
   }
   if (!OPEN && wm == 0) big8_bar();
@@ -1660,6 +1786,9 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
   const int G = gridDim.x;
   const int nk = p.K / 64;
   const int xg = p.xgroups;
+  // the two-phase K-tile for the LN-folded FC1 + GELU kernels (big8_ktile2)
+  constexpr bool KT2 = (FL & EPI_LNIN) && (FL & (EPI_GELU | EPI_GELU_ERF)) &&
+                       !(FL & (EPI_RESID | EPI_HM | EPI_STATS | EPI_GATHER | EPI_SPLIT));
   int tm, tn;
   pers_tile(tile, G, p.ntiles, xg, total, tm, tn);
   if (DBG == 5) {  // experiment: stagger the blocks' start
@@ -1715,14 +1844,14 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
                           ntn * BIG_BN, pre1, mid, {}, {}, par);
       else
         big8_loop<PERS_X, true, decltype(pre1), decltype(mid), (ER > 0 ? 4 : 0), decltype(last),
-                  (ER > 1 ? 4 : 0), decltype(last3), P>(
+                  (ER > 1 ? 4 : 0), decltype(last3), P, KT2>(
             p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM, ntn * BIG_BN, pre1, mid,
             last, last3, par);
       stamp(1);
       if (has_next && !cont) big8_prologue(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nk);
     } else {
       big8_loop<PERS_X, false, NoOp, NoOp, (ER > 0 ? 4 : 0), decltype(last), (ER > 1 ? 4 : 0),
-                decltype(last3), P>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
+                decltype(last3), P, KT2>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
                                     ntn * BIG_BN, {}, {}, last, last3, par);
       stamp(1);
       pers_coef<FL>(p, smem, tid);
