@@ -91,6 +91,13 @@ def parse():
                     help="strong scaling: shard ONE global batch of this many images over the ranks")
     ap.add_argument("--dist-timeout", type=float, default=300.0,
                     help="process-group (RCCL) timeout in seconds")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1: nccl (= RCCL over xGMI, one GPU per "
+                         "rank) or gloo (host staging; ranks may share a GPU, so the N > 1 code "
+                         "path runs on a one-GPU box: a plumbing check, not a scaling number)")
+    ap.add_argument("--dump-logits", default="",
+                    help="rank 0 writes the last step's gathered [global batch, classes] fp32 "
+                         "logits to this .npy file (the multi-rank parity test)")
     return ap.parse_args()
 
 
@@ -207,13 +214,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
+    ndev = torch.cuda.device_count()
+    if local_rank >= ndev and not (world > 1 and args.dist_backend == "gloo"):
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local_rank} but {ndev} visible GPU(s) "
+                         "(RCCL needs one GPU per rank; --dist-backend gloo may share them)")
+    dev_index = local_rank % max(ndev, 1)
+    torch.cuda.set_device(dev_index)
     dist = None
+    gloo = world > 1 and args.dist_backend == "gloo"
     if world > 1:
         import datetime
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank),
-                                timeout=datetime.timedelta(seconds=args.dist_timeout))
+        if gloo:
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=args.dist_timeout))
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index),
+                                    timeout=datetime.timedelta(seconds=args.dist_timeout))
 
     if args.probe_only:
         from edgevisiontransformer_amd.modeling.models.vit import _cfg_for
@@ -251,18 +267,22 @@ def main():
         g = torch.Generator(device="cuda").manual_seed(1000 + rank)
         img = torch.randn((B, *shape), generator=g, device="cuda", dtype=torch.float32)
     logits = torch.empty((max(B, 1), model.num_classes), device="cuda", dtype=torch.float32)
-    gathered = torch.empty((world * B, model.num_classes), device="cuda") if world > 1 and not strong else None
+    gathered = None
+    if world > 1 and not strong:  # gloo moves host tensors (shard.gather_logits stages the same way)
+        gathered = torch.empty((world * B, model.num_classes), device="cpu" if gloo else "cuda")
+    last = {}
 
     def local_forward(x):
         return model.forward_into(x, logits[: x.shape[0]])
 
     def step():
         if strong:
-            shard.sharded_forward(local_forward, gimg, world, rank)
+            last["logits"] = shard.sharded_forward(local_forward, gimg, world, rank)
         else:
             model.forward_into(img, logits)
             if world > 1:
-                dist.all_gather_into_tensor(gathered, logits)
+                dist.all_gather_into_tensor(gathered, logits.cpu() if gloo else logits)
+            last["logits"] = gathered if world > 1 else logits
 
     for _ in range(args.warmup):
         step()
@@ -278,10 +298,12 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], device="cuda", dtype=torch.float64)
+        t = torch.tensor([el], device="cpu" if gloo else "cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     ok = bool(torch.isfinite(logits[:B]).all().item())
+    if args.dump_logits and rank == 0:
+        np.save(args.dump_logits, last["logits"].float().cpu().numpy())
 
     gflop_img = model.cfg.gflop_per_image()
     imgs_per_s = G * args.steps / el
@@ -323,9 +345,10 @@ def main():
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(args.model, args.cpu_seconds)
     if rank == 0:
+        coll = "gloo all-gather of logits, ranks sharing GPUs" if gloo else "RCCL all-gather of logits"
         par = "dp1" if world == 1 else (
-            f"dp{world} (one global batch of {G} sharded {B}-{cap} per GPU, RCCL all-gather of logits)"
-            if strong else f"dp{world} (batch shard, RCCL all-gather of logits)")
+            f"dp{world} (one global batch of {G} sharded {B}-{cap} per GPU, {coll})"
+            if strong else f"dp{world} (batch shard, {coll})")
         out = {
             "metric": METRIC if args.model == "deit_base" else f"images/sec {args.model} bs={B}",
             "value": round(imgs_per_s, 2), "unit": "images/s", "n_gpus": world,
@@ -345,6 +368,12 @@ def main():
                                "gflop_per_image": round(gflop_img, 3)},
             "roofline": roof, "cpu_baseline": cpu, "logits_finite": ok,
         }
+        if world > 1:
+            out["dist_backend"] = args.dist_backend
+            out["devices"] = ndev
+            if gloo:
+                out["note"] = ("gloo plumbing run of the N > 1 code path (ranks may share a GPU): "
+                               "not a scaling measurement")
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -111,6 +111,7 @@ SIGNATURES = {
     "evt_graph_capture": (_I, [_P, _P, _I, _P, _P]),
     "evt_graph_launch": (_I, [_P, _P]),
     "evt_set_gemm_variant": (_I, [_I]),
+    "evt_model_qkv_layout": (_I, [_P, ctypes.POINTER(_I)]),
     "evt_model_profile": (_I, [_P, _I]),
     "evt_model_profile_read": (_I, [_P, _P, _P]),
     "evt_model_profile_work": (_I, [_P, _P, _P]),

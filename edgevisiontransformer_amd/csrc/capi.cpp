@@ -115,6 +115,7 @@ struct evt_model {
   // QKV output head-major where the GEMM supports it (run_encoder); EVT_QKV_LAYOUT=token at model
   // creation keeps the token-major layout (the A/B and bitwise-equality tests)
   bool headmajor = qkv_headmajor_default();
+  int hm_layers = 0;         // encoder layers whose QKV stored head-major in the last forward
   bool patch_cm = false;     // ViT: channel-major patch vectors / patch weight rows
   void* qa = nullptr;        // MX8: [rows][max(Dpad, innerpad)] e4m3 A operand (LN out / attn out)
   uint32_t* sa = nullptr;    // MX8: its scales [pad/128][rows]
@@ -531,6 +532,7 @@ int dense_head(const evt_model* m, const DenseW& w, const DenseCall& c, hipStrea
 int run_encoder(evt_model* m, int B, hipStream_t s) {
   const int D = m->D, T = m->sh.T, rows = B * T;
   const float log2e = 1.4426950408889634f;
+  m->hm_layers = 0;
   for (const Layer& L : m->layers) {
     const float scale_log2 = log2e / std::sqrt((float)L.hd);  // h_k^-0.5 (attention.py:13)
     // qkv head-major ([B][heads][q | k | v][T][64], EPI_HM) where the QKV GEMM takes the
@@ -551,6 +553,7 @@ int run_encoder(evt_model* m, int B, hipStream_t s) {
         if (gemm_headmajor_ok(m->dtype, h.flags, dense_params(m, L.qkv, h))) {
           c = h;
           hm = true;
+          ++m->hm_layers;
         }
       }
       EVT_RC(dense(m, L.qkv, c, s));
@@ -824,6 +827,9 @@ int evt_query_workspace(const evt_vit_desc* desc, int batch, size_t* bytes) {
 
 int evt_model_destroy(evt_model* m) {
   if (!m) return EVT_OK;
+  // forwards enqueued on any stream may still read the workspace / weights: wait for the device
+  // before freeing (hipFree would also synchronise, but only implicitly)
+  (void)hipDeviceSynchronize();
   if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
   if (m->graph) (void)hipGraphDestroy(m->graph);
   for (hipEvent_t e : m->prof_ev) (void)hipEventDestroy(e);
@@ -1232,6 +1238,12 @@ int evt_model_profile_read(evt_model* m, float* us, int* launches) {
     us[m->prof_role[i]] += 1000.f * ms;
     launches[m->prof_role[i]] += 1;
   }
+  return EVT_OK;
+}
+
+int evt_model_qkv_layout(const evt_model* m, int* headmajor_layers) {
+  if (!m || !headmajor_layers) return fail(EVT_EINVAL, "null argument");
+  *headmajor_layers = m->hm_layers;
   return EVT_OK;
 }
 

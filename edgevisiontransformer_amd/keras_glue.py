@@ -103,29 +103,46 @@ def ordered_keras_variables(keras_vit, image_size: int = 224) -> List[np.ndarray
     return _checked(keras_vit_params(keras_vit), keras_vit_config(keras_vit, image_size))
 
 
-def keras_weight_names(cfg: ViTConfig, own_first: bool = False) -> List[str]:
+def keras_weight_names(cfg: ViTConfig, own_first: bool = False,
+                       head_first: bool = False) -> List[str]:
     """vit_param_shapes names in Keras tracking order (model.weights / get_weights()): the
     sub-layers (patch_to_embedding, the blocks, mlp_head) in attribute order, the model's own
-    pos_embedding / cls_token after them (tf.keras Model) or before them (own_first)."""
-    names = ["patch_w", "patch_b"]
+    pos_embedding / cls_token after them (tf.keras Model) or before them (own_first).
+    head_first: the ViT_Pruned order. Its constructor assigns a new `self.transformer` after
+    `ViT.__init__` (reference vit.py:74); Keras untracks the replaced block and appends the new
+    one, so the blocks follow mlp_head: patch_to_embedding, mlp_head, transformer."""
+    blocks = []
     for i in range(cfg.depth):
-        names += [f"l{i}.{n}" for n in ("ln1_g", "ln1_b", "qkv_w", "out_w", "out_b", "ln2_g",
-                                        "ln2_b", "fc1_w", "fc1_b", "fc2_w", "fc2_b")]
-    names += ["head1_w", "head1_b", "head2_w", "head2_b"]
+        blocks += [f"l{i}.{n}" for n in ("ln1_g", "ln1_b", "qkv_w", "out_w", "out_b", "ln2_g",
+                                         "ln2_b", "fc1_w", "fc1_b", "fc2_w", "fc2_b")]
+    head = ["head1_w", "head1_b", "head2_w", "head2_b"]
+    names = ["patch_w", "patch_b"] + (head + blocks if head_first else blocks + head)
     return ["pos", "cls"] + names if own_first else names + ["pos", "cls"]
 
 
 def reorder_keras_weight_list(weights: Sequence, cfg: ViTConfig) -> List[np.ndarray]:
-    """`model.get_weights()` of a reference ViT (Keras tracking order) -> the C-ABI order."""
+    """`model.get_weights()` of a reference ViT or ViT_Pruned (Keras tracking order) -> the C-ABI
+    order. The order is read off the list itself: the [1, 1, dim] cls_token at the front or the
+    end (the model's own variables before / after its sub-layers), and after patch_b either the
+    rank-1 [dim] LayerNorm gamma of block 0 (ViT) or the rank-2 [dim, mlp_dim] kernel of the first
+    mlp_head Dense (ViT_Pruned's re-tracked transformer, keras_weight_names)."""
     n = len(keras_weight_names(cfg))
     if len(weights) != n:
         raise ValueError(f"{len(weights)} Keras weights, the config has {n}")
     if np.ndim(weights[1]) == 3:
-        names = keras_weight_names(cfg, own_first=True)
+        own_first = True
     elif np.ndim(weights[-1]) == 3:
-        names = keras_weight_names(cfg)
+        own_first = False
     else:
         raise ValueError("no [1, 1, dim] cls_token at either end of the weight list")
+    after_patch = weights[4 if own_first else 2]
+    if cfg.depth == 0 or np.ndim(after_patch) == 2:
+        head_first = cfg.depth > 0
+    elif np.ndim(after_patch) == 1:
+        head_first = False
+    else:
+        raise ValueError(f"unexpected rank-{np.ndim(after_patch)} weight after patch_to_embedding")
+    names = keras_weight_names(cfg, own_first=own_first, head_first=head_first)
     p = {nm: _np(w) for nm, w in zip(names, weights)}
     p["cls"] = p["cls"].reshape(-1)  # [1, 1, dim] (vit.py:24-29)
     return _checked(p, cfg)

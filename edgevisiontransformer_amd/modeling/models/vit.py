@@ -156,6 +156,14 @@ class ViT:
         self._handle = out.value
         self._max_batch = max_batch
 
+    def qkv_headmajor_layers(self) -> int:
+        """Encoder layers whose QKV output was stored head-major in the last forward
+        (evt_model_qkv_layout; diagnostics for the layout-equality tests)."""
+        out = ctypes.c_int()
+        _lib.check(_lib.load_library().evt_model_qkv_layout(ctypes.c_void_p(self._handle),
+                                                             ctypes.byref(out)))
+        return out.value
+
     def workspace_bytes(self, batch: int) -> int:
         lib = _lib.load_library()
         out = ctypes.c_size_t()

@@ -44,9 +44,11 @@ def gather_logits(local: torch.Tensor, global_batch: int, world: int,
         return local
     C = local.shape[1]
     cap = -(-global_batch // world)
-    buf = torch.zeros((cap, C), dtype=local.dtype, device=local.device)
-    buf[: local.shape[0]] = local
-    out = torch.empty((world * cap, C), dtype=local.dtype, device=local.device)
+    # gloo moves host tensors: stage device logits through the host (RCCL gathers in place)
+    dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else local.device
+    buf = torch.zeros((cap, C), dtype=local.dtype, device=dev)
+    buf[: local.shape[0]] = local.to(dev)
+    out = torch.empty((world * cap, C), dtype=local.dtype, device=dev)
     if timeout is None:
         dist.all_gather_into_tensor(out, buf, group=group)
     else:

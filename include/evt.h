@@ -114,7 +114,8 @@ int evt_graph_launch(evt_model* model, void* stream);
 /* Bytes of device workspace evt_vit_create allocates for `batch` images. */
 int evt_query_workspace(const evt_vit_desc* desc, int batch, size_t* bytes);
 
-/* Release everything the handle owns. NULL is accepted. */
+/* Release everything the handle owns, after waiting for the device (forwards still in flight on
+ * any stream finish first). NULL is accepted. */
 int evt_model_destroy(evt_model* model);
 
 /* ---- op-level entry points (one per hot-path kernel; used by the parity tests) ---------- */
@@ -433,6 +434,13 @@ int evt_attention_mx8(const void* qkv, int64_t ldq, void* q8, int64_t ldq8, uint
  * EVT_LAB=1 (-DEVT_GEMM_LAB) also accept the ablation / timeline variants 10, 11, 13, 15, 17-25,
  * 106, 108; other values return EVT_EINVAL. */
 int evt_set_gemm_variant(int variant);
+
+/* Number of encoder layers whose QKV GEMM stored its output head-major ([B][H][q | k | v][T][64],
+ * the persistent kernel's EPI_HM store) in the handle's last forward; 0 when every layer kept the
+ * token-major (qkv h d) columns of attention.py:20 (EVT_QKV_LAYOUT=token, f32, head size != 64 or
+ * a problem the persistent kernel does not take). Lets the layout-equality tests assert which
+ * path ran. */
+int evt_model_qkv_layout(const evt_model* m, int* headmajor_layers);
 
 #ifdef __cplusplus
 }

@@ -90,14 +90,18 @@ def test_batch_independence(gpu, dtype):
     assert torch.equal(torch.roll(auto, 11, 0), rolled)
 
 
-@pytest.mark.parametrize("which,batch", [("deit_tiny", 64), ("deit_base", 20), ("pruned", 48),
-                                         ("deit_tiny", 3)])
-def test_qkv_head_major_bitwise(gpu, monkeypatch, which, batch):
+@pytest.mark.parametrize("which,batch,hm_layers", [
+    ("deit_tiny", 64, 12), ("deit_base", 20, 12), ("pruned", 48, 6), ("deit_tiny", 3, 0),
+    # fewer than 128 tokens per image: the per-row image / token decode of the EPI_HM store (37
+    # and 50 tokens; images straddle lanes' 16-row runs and the M edge of the last tile)
+    ("tiny96", 300, 12), ("tiny112", 260, 12)])
+def test_qkv_head_major_bitwise(gpu, monkeypatch, which, batch, hm_layers):
     """The head-major qkv layout (the QKV GEMM's EPI_HM store + the attention's slice strides; used
     where that GEMM runs the persistent kernel: every case here but the 3-image one) against the
     token-major layout (EVT_QKV_LAYOUT=token at model creation): the same arithmetic at other
     addresses, so the logits agree bit for bit. 'pruned': per-layer head counts 1-3 (QKV widths
-    192-576, column-padded tiles)."""
+    192-576, column-padded tiles). `hm_layers`: the layers whose QKV must have stored head-major
+    (evt_model_qkv_layout), so a silent fallback to token-major cannot pass as equality."""
     from edgevisiontransformer_amd.modeling.models import vit
 
     def build():
@@ -105,14 +109,23 @@ def test_qkv_head_major_bitwise(gpu, monkeypatch, which, batch):
             return ViT_Pruned(dim=192, depth=6, heads=3, mlp_dim=768, head_size=64,
                               prune_encoding="layerwise_h1-d0.5_h3-d1.0_h2-d0.3_h3-d0.7_h1-d1.0_h2-d0.2",
                               dtype="bf16", seed=12, device=gpu)
+        if which.startswith("tiny"):
+            return ViT(image_size=int(which[4:]), patch_size=16, dim=192, depth=12, heads=3,
+                       mlp_dim=768, dtype="bf16", seed=12, device=gpu)
         return getattr(vit, f"get_{which}")(dtype="bf16", seed=12, device=gpu)
 
-    img = torch.from_numpy(make_images(batch, seed=21)).to(gpu)
+    size = int(which[4:]) if which.startswith("tiny") else 224
+    img = torch.from_numpy(make_images(batch, seed=21, image_size=size)).to(gpu)
     monkeypatch.setenv("EVT_QKV_LAYOUT", "token")
-    tok = build()(img)
-    monkeypatch.delenv("EVT_QKV_LAYOUT")
-    hm = build()(img)
+    mt = build()
+    tok = mt(img)
     torch.cuda.synchronize()
+    assert mt.qkv_headmajor_layers() == 0
+    monkeypatch.delenv("EVT_QKV_LAYOUT")
+    mh = build()
+    hm = mh(img)
+    torch.cuda.synchronize()
+    assert mh.qkv_headmajor_layers() == hm_layers
     assert torch.isfinite(hm).all()
     assert torch.equal(tok, hm)
 

