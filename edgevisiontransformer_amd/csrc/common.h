@@ -192,6 +192,18 @@ __device__ __forceinline__ void glds16(const void* gsrc, EVT_LDS void* lds_base)
   __builtin_amdgcn_global_load_lds(gsrc, lds_base, 16, 0, 0);
 }
 
+// glds16 through the SGPR-base form (global_load_lds_dwordx4 v_off, s[base]): a wave-uniform
+// 64-bit base plus a per-lane 32-bit offset, so a K-loop advances the base in SALU and keeps
+// loop-invariant 32-bit lane offsets instead of one 64-bit VALU address add per piece (hipcc only
+// emits the 64-bit vaddr form for the builtin). The wait state between the M0 write and the LDS
+// DMA (as hipcc emits it) is the s_nop. hipcc does not count these loads: every consumer retires
+// them with explicit s_waitcnt vmcnt (big8_* counted waits).
+__device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, EVT_LDS void* lds_base) {
+  const uint32_t m = (uint32_t)(uintptr_t)lds_base;
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+               :: "v"(voff), "s"(sbase), "s"(m) : "memory", "m0");
+}
+
 __device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 }  // namespace evt

@@ -662,13 +662,15 @@ __device__ __forceinline__ void big8_stage(const P& p, char* smem, int wave, int
       const int g = wave * Gm::AI + i, gpw = Gm::WR / 16;
       const int row = (g / gpw) * Gm::WR + h * (Gm::WR / 2) + (g % gpw) * 8;
       const int gm = min(m0 + row + srow, p.M - 1);
-      glds16((const char*)p.A + (int64_t)gm * (p.lda * 2) + koff, base + row * ROWB);
+      glds16s((const char*)p.A + (int64_t)m0 * (p.lda * 2) + T * ROWB,
+              (uint32_t)((gm - m0) * (p.lda * 2)) + ((sslot ^ srow) << 4), base + row * ROWB);
     };
     auto w_ins = [&](int h, int i) {  // W n-half h, instruction i of WI: rows wn*WC + h*WC/2 + ..
       const int g = wave * Gm::WI + i, gpw = Gm::WC / 16;
       const int row = (g / gpw) * Gm::WC + h * (Gm::WC / 2) + (g % gpw) * 8;
-      glds16((const char*)p.W + (int64_t)(n0 + row + srow) * (p.ldw * 2) + koff,
-             base + Gm::A_TILE + row * ROWB);
+      glds16s((const char*)p.W + (int64_t)n0 * (p.ldw * 2) + T * ROWB,
+              (uint32_t)((row + srow) * (p.ldw * 2)) + ((sslot ^ srow) << 4),
+              base + Gm::A_TILE + row * ROWB);
     };
     auto ins = [&](int q) {  // instruction q (0..7) of the K-tile's sequence
       if (q < Gm::AI) a_ins(0, q);
@@ -690,12 +692,14 @@ __device__ __forceinline__ void big8_stage(const P& p, char* smem, int wave, int
         glds16(gather_addr<1>(p, gm, T * 64 + ((sslot ^ srow) << 3)), base + row * ROWB);
       else if constexpr (std::is_same<P, UnfoldParams>::value)
         glds16(gather_addr<2>(p, gm, T * 64 + ((sslot ^ srow) << 3)), base + row * ROWB);
-      else
-        glds16((const char*)p.A + (int64_t)gm * (p.lda * 2) + koff, base + row * ROWB);
+      else  // SGPR base = the tile's first row at K-tile T, 32-bit lane offsets (glds16s)
+        glds16s((const char*)p.A + (int64_t)m0 * (p.lda * 2) + T * ROWB,
+                (uint32_t)((gm - m0) * (p.lda * 2)) + ((sslot ^ srow) << 4), base + row * ROWB);
     } else {
       const int row = ((r >> 5) << 6) + (r & 31) + (j == 2 ? 32 : 0);
-      glds16((const char*)p.W + (int64_t)(n0 + row + srow) * (p.ldw * 2) + koff,
-             base + BIG_TILE + row * ROWB);
+      glds16s((const char*)p.W + (int64_t)n0 * (p.ldw * 2) + T * ROWB,
+              (uint32_t)((row + srow) * (p.ldw * 2)) + ((sslot ^ srow) << 4),
+              base + BIG_TILE + row * ROWB);
     }
   }
 }
@@ -1778,8 +1782,12 @@ __device__ __forceinline__ bool pers_tile(int t, int G, int ntiles, int xgroups,
 template <int FL, int DBG, bool PADN, typename P = GemmParams>
 __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* smem) {
   // a quarter of the residual before the last K-tile (out-proj 160 -> 153 us); DBG 20: A/B without
+#ifdef EVT_ER1
+  constexpr int ER = ((FL & EPI_RESID) != 0) ? 1 : 0;
+#else
   constexpr int ER = ((FL & EPI_RESID) != 0 && DBG != 7 && DBG != 20 && DBG != 18)
                          ? (DBG == 21 ? 1 : 2) : 0;  // DBG 21: A/B with one quarter
+#endif
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -1787,8 +1795,14 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
   const int nk = p.K / 64;
   const int xg = p.xgroups;
   // the two-phase K-tile for the LN-folded FC1 + GELU kernels (big8_ktile2)
+#ifdef EVT_KT2_ALL
+  constexpr bool KT2 = true;
+#elif defined(EVT_KT2_FC1)
   constexpr bool KT2 = (FL & EPI_LNIN) && (FL & (EPI_GELU | EPI_GELU_ERF)) &&
                        !(FL & (EPI_RESID | EPI_HM | EPI_STATS | EPI_GATHER | EPI_SPLIT));
+#else
+  constexpr bool KT2 = !(FL & (EPI_RESID | EPI_GATHER | EPI_SPLIT));
+#endif
   int tm, tn;
   pers_tile(tile, G, p.ntiles, xg, total, tm, tn);
   if (DBG == 5) {  // experiment: stagger the blocks' start
