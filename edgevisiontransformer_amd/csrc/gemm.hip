@@ -1782,12 +1782,8 @@ __device__ __forceinline__ bool pers_tile(int t, int G, int ntiles, int xgroups,
 template <int FL, int DBG, bool PADN, typename P = GemmParams>
 __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* smem) {
   // a quarter of the residual before the last K-tile (out-proj 160 -> 153 us); DBG 20: A/B without
-#ifdef EVT_ER1
-  constexpr int ER = ((FL & EPI_RESID) != 0) ? 1 : 0;
-#else
   constexpr int ER = ((FL & EPI_RESID) != 0 && DBG != 7 && DBG != 20 && DBG != 18)
                          ? (DBG == 21 ? 1 : 2) : 0;  // DBG 21: A/B with one quarter
-#endif
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -1795,14 +1791,10 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
   const int nk = p.K / 64;
   const int xg = p.xgroups;
   // the two-phase K-tile for the LN-folded FC1 + GELU kernels (big8_ktile2)
-#ifdef EVT_KT2_ALL
-  constexpr bool KT2 = true;
-#elif defined(EVT_KT2_FC1)
+  // (round 6, with the SGPR-base DMA: the two-phase K-tile on every non-residual instance, where
+  // it no longer spills, measured equal to this rule: QKV 311.8 vs 311.9 us, r6c A/B)
   constexpr bool KT2 = (FL & EPI_LNIN) && (FL & (EPI_GELU | EPI_GELU_ERF)) &&
                        !(FL & (EPI_RESID | EPI_HM | EPI_STATS | EPI_GATHER | EPI_SPLIT));
-#else
-  constexpr bool KT2 = !(FL & (EPI_RESID | EPI_GATHER | EPI_SPLIT));
-#endif
   int tm, tn;
   pers_tile(tile, G, p.ntiles, xg, total, tm, tn);
   if (DBG == 5) {  // experiment: stagger the blocks' start
