@@ -204,6 +204,17 @@ __device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, EVT_LD
                :: "v"(voff), "s"(sbase), "s"(m) : "memory", "m0");
 }
 
+// Two glds16s pieces whose LDS destinations are 1 KiB apart under one M0 write: the second uses
+// instruction offset 1024, which global_load_lds applies to the LDS and the global address alike
+// (its lane offset voff1 is the global offset minus 1024). Issue order: voff0's piece first.
+__device__ __forceinline__ void glds16s_pair(const void* sbase, uint32_t voff0, uint32_t voff1,
+                                             EVT_LDS void* lds_base) {
+  const uint32_t m = (uint32_t)(uintptr_t)lds_base;
+  asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %2\n\t"
+               "global_load_lds_dwordx4 %1, %2 offset:1024"
+               :: "v"(voff0), "v"(voff1), "s"(sbase), "s"(m) : "memory", "m0");
+}
+
 __device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 }  // namespace evt

@@ -652,6 +652,11 @@ __device__ __forceinline__ void big8_stage(const P& p, char* smem, int wave, int
   typedef Geo<P> Gm;
   const int srow = lane >> 3, sslot = lane & 7;
   EVT_LDS char* base = (EVT_LDS char*)smem + ((T ^ par) & 1) * BIG_STAGE;
+#ifdef EVT_ABL_KT0  // lab ablation: every K-tile DMAs K-tile 0's bytes (cache-resident; wrong results)
+  const int Tg = 0;
+#else
+  const int Tg = T;
+#endif
   const int64_t koff = (int64_t)T * ROWB + ((sslot ^ srow) << 4);
   if constexpr (Gm::BM != 256) {
     // general geometry: a K-tile's 8 DMA instructions per wave in the region order of the 256 x 256
@@ -662,13 +667,13 @@ __device__ __forceinline__ void big8_stage(const P& p, char* smem, int wave, int
       const int g = wave * Gm::AI + i, gpw = Gm::WR / 16;
       const int row = (g / gpw) * Gm::WR + h * (Gm::WR / 2) + (g % gpw) * 8;
       const int gm = min(m0 + row + srow, p.M - 1);
-      glds16s((const char*)p.A + (int64_t)m0 * (p.lda * 2) + T * ROWB,
+      glds16s((const char*)p.A + (int64_t)m0 * (p.lda * 2) + Tg * ROWB,
               (uint32_t)((gm - m0) * (p.lda * 2)) + ((sslot ^ srow) << 4), base + row * ROWB);
     };
     auto w_ins = [&](int h, int i) {  // W n-half h, instruction i of WI: rows wn*WC + h*WC/2 + ..
       const int g = wave * Gm::WI + i, gpw = Gm::WC / 16;
       const int row = (g / gpw) * Gm::WC + h * (Gm::WC / 2) + (g % gpw) * 8;
-      glds16s((const char*)p.W + (int64_t)n0 * (p.ldw * 2) + T * ROWB,
+      glds16s((const char*)p.W + (int64_t)n0 * (p.ldw * 2) + Tg * ROWB,
               (uint32_t)((row + srow) * (p.ldw * 2)) + ((sslot ^ srow) << 4),
               base + Gm::A_TILE + row * ROWB);
     };
@@ -682,6 +687,29 @@ __device__ __forceinline__ void big8_stage(const P& p, char* smem, int wave, int
     ins(2 * j + 1);
     return;
   }
+#ifndef EVT_GLDS_UNPAIRED
+  if constexpr (!std::is_same<P, MergeParams>::value && !std::is_same<P, UnfoldParams>::value) {
+    // the wave's two pieces of the region are 8 rows = 1 KiB apart in LDS: one M0 for both, the
+    // second at instruction offset 1024 (applied to the LDS and the global address alike; the
+    // SGPR base moves down 1 KiB so that no lane offset goes negative)
+    const int r = wave * 16;
+    const uint32_t swz = (uint32_t)((sslot ^ srow) << 4);
+    if (j == 0 || j == 3) {
+      const int row = (r & 63) + ((r >> 6) << 7) + (j == 3 ? 64 : 0);
+      const int gm0 = min(m0 + row + srow, p.M - 1), gm1 = min(m0 + row + 8 + srow, p.M - 1);
+      glds16s_pair((const char*)p.A + (int64_t)m0 * (p.lda * 2) + Tg * ROWB - 1024,
+                   (uint32_t)((gm0 - m0) * (p.lda * 2)) + swz + 1024,
+                   (uint32_t)((gm1 - m0) * (p.lda * 2)) + swz, base + row * ROWB);
+    } else {
+      const int row = ((r >> 5) << 6) + (r & 31) + (j == 2 ? 32 : 0);
+      glds16s_pair((const char*)p.W + (int64_t)n0 * (p.ldw * 2) + Tg * ROWB - 1024,
+                   (uint32_t)((row + srow) * (p.ldw * 2)) + swz + 1024,
+                   (uint32_t)((row + 8 + srow) * (p.ldw * 2)) + swz,
+                   base + BIG_TILE + row * ROWB);
+    }
+    return;
+  }
+#endif
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int r = (wave * 2 + i) * 8;  // region row of this wave-instruction (8 rows)
@@ -693,11 +721,11 @@ __device__ __forceinline__ void big8_stage(const P& p, char* smem, int wave, int
       else if constexpr (std::is_same<P, UnfoldParams>::value)
         glds16(gather_addr<2>(p, gm, T * 64 + ((sslot ^ srow) << 3)), base + row * ROWB);
       else  // SGPR base = the tile's first row at K-tile T, 32-bit lane offsets (glds16s)
-        glds16s((const char*)p.A + (int64_t)m0 * (p.lda * 2) + T * ROWB,
+        glds16s((const char*)p.A + (int64_t)m0 * (p.lda * 2) + Tg * ROWB,
                 (uint32_t)((gm - m0) * (p.lda * 2)) + ((sslot ^ srow) << 4), base + row * ROWB);
     } else {
       const int row = ((r >> 5) << 6) + (r & 31) + (j == 2 ? 32 : 0);
-      glds16s((const char*)p.W + (int64_t)n0 * (p.ldw * 2) + T * ROWB,
+      glds16s((const char*)p.W + (int64_t)n0 * (p.ldw * 2) + Tg * ROWB,
               (uint32_t)((row + srow) * (p.ldw * 2)) + ((sslot ^ srow) << 4),
               base + BIG_TILE + row * ROWB);
     }
