@@ -2473,6 +2473,12 @@ hipError_t launch_big(const GemmParams& p, hipStream_t s) {
 }
 
 int g_num_cus = 0;
+// persistent grid balancing (launch_pers): 1 = for launches of 2-4 tile rounds (default),
+// 0 = never, 2 = always; EVT_GRID_BALANCE, read once (A/B switch)
+const int g_grid_balance = [] {
+  const char* e = std::getenv("EVT_GRID_BALANCE");
+  return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 1;
+}();
 
 int num_cus() {
   if (!g_num_cus) {
@@ -2536,6 +2542,14 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
   const int total = ((p.M + BIG_BM - 1) / BIG_BM) * q.ntiles;
   int G = min(total, g_gemm_variant == 10 ? 8 : g_num_cus);  // 10: few blocks, many tiles each
   if (G >= 8 && total > G) G &= ~7;
+  // 2-4 tile rounds: as few blocks as keep the round count (multiple of 8), every block the same
+  // number of tiles. Measured round 6 (r6f, alternating): DeiT-base at 64 images 22.67k -> 23.30k
+  // img/s (FC1 600 tiles: 200 blocks x 3 instead of 256 with 88 taking a third; QKV 450: 232 x 2),
+  // the CUs left idle let the busy ones hold a higher clock; at 512 images (>= 5 rounds) -0.3 %,
+  // not applied there. EVT_GRID_BALANCE=0 / 2: never / always (A/B)
+  const int rounds = (total + G - 1) / G;
+  if (total > G && G >= 8 && (g_grid_balance == 2 || (g_grid_balance == 1 && rounds <= 4)))
+    G = min(G, (((total + rounds - 1) / rounds) + 7) & ~7);
   // one round (one block per tile): up to a multiple of 8 blocks (the surplus exits at once) so
   // that the XCD-major start order applies and an m-panel's n-tiles run on one XCD, its A panel
   // fetched once into that L2 (DeiT-base FC2 at 64 images: 150 tiles, 3 per 1.5 MB A panel; in
