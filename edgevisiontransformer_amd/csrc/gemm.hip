@@ -2530,10 +2530,7 @@ bool use_pers(const GemmParams& p, int flags) {
 // two groups of four XCDs and the launch has more than one round (FC1 of the D = 768 models: 12
 // panels -> 6 per group; measured round 4: one group 484.5 us, two 479.9, four 479.3 per FC1 launch)
 int pers_xgroups(int ntiles, int G, int total) {
-  // the walk arithmetic needs whole XCD groups: G a multiple of 8 (blocks b, b + 8, ... share an
-  // XCD); bijective for every such G with 2 groups (checked by enumeration, round 6, for the
-  // balanced grids of launch_pers: e.g. DeiT-base FC1 at 64 images, 200 blocks)
-  if (G % 8 || G < 64 || total <= G) return 1;
+  if (G != 256 || total <= G) return 1;  // the walk arithmetic assumes 8 XCDs of 32 blocks
   return (ntiles % 2 == 0 && ntiles / 2 >= 3) ? 2 : 1;
 }
 
