@@ -1603,7 +1603,7 @@ int evt_patch_merge(int dtype, const void* x, int64_t ldx, int B, int R, int C, 
 
 int evt_set_gemm_variant(int variant) {
   if (!gemm_variant_supported(variant))
-    return fail(EVT_EINVAL, "variant must be 0, 1, 2, 6, 8, 9, 16, 30 or 31 (lab builds: also "
+    return fail(EVT_EINVAL, "variant must be 0, 1, 2, 6, 8, 9, 16, 30, 31 or 36 (lab builds: also "
                             "10, 11, 13, 15, 17-25, 106, 108)");
   gemm_set_variant(variant);
   return EVT_OK;

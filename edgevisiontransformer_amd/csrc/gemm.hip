@@ -507,7 +507,8 @@ int num_cus();
 bool use_big(const GemmParams& p, int flags) {
   if ((p.ntiles * GEMM_BN) % BIG_BN) return false;
   if (!(flags & EPI_OUT_F32) && p.vec_ok < 2) return false;  // big epilogue: 16-B bf16 stores only
-  const int v = g_gemm_variant == 31 ? 0 : g_gemm_variant;  // 31: automatic without 128 x 384
+  // 31: automatic without 128 x 384, 36: automatic without grid balancing (launch_pers)
+  const int v = (g_gemm_variant == 31 || g_gemm_variant == 36) ? 0 : g_gemm_variant;
   if (v == 1) return false;
   if (v >= 2) return true;
   // 256x256 tiles unless their rounds cost more: time in 256-tile units, the 128x128 kernel at a
@@ -2514,7 +2515,7 @@ bool gemm_lab_pers_variant(int v) {
 
 bool use_pers(const GemmParams& p, int flags) {
   const int v = g_gemm_variant;
-  if (v != 0 && v != 9 && v != 16 && v != 31 && !gemm_lab_pers_variant(v))
+  if (v != 0 && v != 9 && v != 16 && v != 31 && v != 36 && !gemm_lab_pers_variant(v))
     return false;
   // timeline variants stamp s_memtime through p.pos: never on the patch GEMM (p.pos = the table)
   if ((v == 13 || v == 15) && (flags & EPI_POS)) return false;
@@ -2546,9 +2547,11 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
   // number of tiles. Measured round 6 (r6f, alternating): DeiT-base at 64 images 22.67k -> 23.30k
   // img/s (FC1 600 tiles: 200 blocks x 3 instead of 256 with 88 taking a third; QKV 450: 232 x 2),
   // the CUs left idle let the busy ones hold a higher clock; at 512 images (>= 5 rounds) -0.3 %,
-  // not applied there. EVT_GRID_BALANCE=0 / 2: never / always (A/B)
+  // not applied there. evt_set_gemm_variant 36: never (the tile -> block assignment only: bitwise
+  // the same outputs); EVT_GRID_BALANCE=0 / 2: never / always (A/B)
   const int rounds = (total + G - 1) / G;
-  if (total > G && G >= 8 && (g_grid_balance == 2 || (g_grid_balance == 1 && rounds <= 4)))
+  const int bal = g_gemm_variant == 36 ? 0 : g_grid_balance;
+  if (total > G && G >= 8 && (bal == 2 || (bal == 1 && rounds <= 4)))
     G = min(G, (((total + rounds - 1) / rounds) + 7) & ~7);
   // one round (one block per tile): up to a multiple of 8 blocks (the surplus exits at once) so
   // that the XCD-major start order applies and an m-panel's n-tiles run on one XCD, its A panel
@@ -2818,6 +2821,7 @@ int device_cus() { return num_cus(); }
 void gemm_set_variant(int v) { g_gemm_variant = v; }
 bool gemm_variant_supported(int v) {
   return v == 0 || v == 1 || v == 2 || v == 6 || v == 8 || v == 9 || v == 16 || v == 30 || v == 31 ||
+         v == 36 ||
          gemm_lab_pers_variant(v)
 #ifdef EVT_GEMM_LAB
          || v == 106 || v == 108

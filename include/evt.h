@@ -430,7 +430,9 @@ int evt_attention_mx8(const void* qkv, int64_t ldq, void* q8, int64_t ldq8, uint
  * kernel's, else 128x128), 1 = always 128x128, 2 / 6 / 8 = non-persistent 256x256 tiles with the
  * plain / interleaved / 8-phase ping-pong main loop whenever the packed width allows, 9 =
  * tile-persistent, 16 = stream-K persistent where it applies, 30 = the 128 x 384 persistent tiles
- * wherever the width allows (multiple of 384), 31 = automatic without them. Builds with
+ * wherever the width allows (multiple of 384), 31 = automatic without them, 36 = automatic with the
+ * persistent grids at one block per CU (no balancing of 2-4-round launches to fewer blocks: the
+ * same tiles and arithmetic, bitwise the same outputs). Builds with
  * EVT_LAB=1 (-DEVT_GEMM_LAB) also accept the ablation / timeline variants 10, 11, 13, 15, 17-25,
  * 106, 108; other values return EVT_EINVAL. */
 int evt_set_gemm_variant(int variant);

@@ -64,7 +64,7 @@ def test_host_validation_codes(lib):
     assert b"lab builds" in lib.evt_last_error()
     for v in (32, 33, 34, 35):  # removed in round 5 (measured-slower lab variants)
         assert lib.evt_set_gemm_variant(v) == _lib.EVT_EINVAL
-    for v in (1, 2, 6, 8, 9, 16, 30, 31, 0):
+    for v in (1, 2, 6, 8, 9, 16, 30, 31, 36, 0):
         assert lib.evt_set_gemm_variant(v) == 0
     assert lib.evt_graph_launch(None, None) == _lib.EVT_EINVAL
     assert lib.evt_graph_capture(None, None, 1, None, None) == _lib.EVT_EINVAL

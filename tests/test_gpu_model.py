@@ -133,6 +133,33 @@ def test_qkv_head_major_bitwise(gpu, monkeypatch, which, batch, hm_layers):
     assert torch.equal(tok, hm)
 
 
+@pytest.mark.parametrize("which,batch", [("deit_base", 64), ("t2t_vit_14", 128)])
+def test_grid_balance_bitwise(gpu, which, batch):
+    """Persistent GEMM launches of 2-4 tile rounds run on fewer blocks with equal tile counts
+    (launch_pers, round 6): only the tile -> block assignment changes, so the logits equal those
+    of one block per CU (evt_set_gemm_variant 36) bit for bit. DeiT-base at 64 images: FC1 600
+    tiles on 200 blocks, QKV 450 on 232; T2T-ViT-14 at 128 images: QKV / FC1 495 tiles on 248."""
+    from edgevisiontransformer_amd import _lib
+    from edgevisiontransformer_amd.modeling.models import t2t_vit, vit
+    if which == "deit_base":
+        m = vit.get_deit_base(dtype="bf16", seed=3, device=gpu)
+        img = torch.from_numpy(make_images(batch, seed=31)).to(gpu)
+    else:
+        m = t2t_vit.get_t2t_vit_14(dtype="bf16", seed=3, device=gpu)
+        img = torch.from_numpy(make_images(batch, seed=31, layout="NHWC")).to(gpu)
+    lib = _lib.load_library()
+    auto = m(img)
+    torch.cuda.synchronize()
+    lib.evt_set_gemm_variant(36)
+    try:
+        flat = m(img)
+        torch.cuda.synchronize()
+    finally:
+        lib.evt_set_gemm_variant(0)
+    assert torch.isfinite(auto).all()
+    assert torch.equal(auto, flat)
+
+
 def test_deit_small_bf16_vs_oracle(gpu):
     from edgevisiontransformer_amd.modeling.models.vit import get_deit_small
     m = get_deit_small(dtype="bf16", seed=4, device=gpu)
