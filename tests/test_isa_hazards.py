@@ -106,3 +106,48 @@ def test_sources_store_wide_only_through_helpers(src):
         if RAW.search(code) and "// LDS" not in line and "EVT_LDS" not in code:
             bad.append(f"{src}:{i}: {line.strip()}")
     assert not bad, "wide stores outside the common.h helpers:\n" + "\n".join(bad)
+
+
+# ---- M0 integrity around the inline-asm LDS-DMA (csrc/common.h glds16s / glds16s_pair) ----------
+# The inline asm writes M0 (the LDS destination of global_load_lds) and lists it as clobbered, but
+# hipcc documents that it may not preserve reserved registers across asm. Every LDS DMA hipcc emits
+# itself (the 64-bit-vaddr form, "v[..], off") must therefore see an M0 write of its own after the
+# last inline-asm DMA block (the saddr form, "vN, s[..]") that precedes it; and M0 must have no
+# other reader (s_movrel / v_movrel / ds_gws / s_sendmsg) in the kernels that use the asm form.
+_M0_WRITE = re.compile(r"^\s*s_\w+\s+m0\b")
+_GLDS_VADDR = re.compile(r"global_load_lds_dword\w*\s+v\[\d+:\d+\],\s*off")
+_GLDS_SADDR = re.compile(r"global_load_lds_dword\w*\s+v\d+,\s*s\[\d+:\d+\]")
+_M0_READERS = re.compile(r"\b(s_movrel\w*|v_movrel\w*|ds_gws\w*|s_sendmsg\w*)\b")
+
+
+def m0_problems(lines):
+    """Indices of hipcc LDS DMAs whose M0 may be an inline-asm block's, and of other M0 readers."""
+    bad, last_write, saddr_since = [], None, False
+    for i, raw in enumerate(lines):
+        l = raw.split("//")[0]
+        if re.match(r"^[0-9a-f]+ <.*>:", raw.strip()):  # a new function (disassembly label)
+            last_write, saddr_since = None, False
+        if _M0_WRITE.match(l):
+            last_write, saddr_since = i, False
+        elif _GLDS_SADDR.search(l):
+            saddr_since = True
+        elif _GLDS_VADDR.search(l) and (last_write is None or saddr_since):
+            bad.append(i)
+        if _M0_READERS.search(l):
+            bad.append(i)
+    return bad
+
+
+def test_m0_scanner_flags_a_stale_m0():
+    asm = ["s_mov_b32 m0, s4", "s_nop 0", "global_load_lds_dwordx4 v1, s[2:3]",
+           "global_load_lds_dwordx4 v[4:5], off"]
+    assert m0_problems(asm) == [3]
+    assert m0_problems(["s_mov_b32 m0, s4", "global_load_lds_dwordx4 v1, s[2:3]",
+                        "s_add_i32 m0, s5, 0x400", "global_load_lds_dwordx4 v[4:5], off"]) == []
+
+
+def test_gemm_m0_integrity(objects, tmp_path):
+    lines = _disassemble(objects["gemm.hip"], tmp_path)
+    assert sum(1 for l in lines if _GLDS_SADDR.search(l)) > 0, "no inline-asm LDS DMA found"
+    bad = m0_problems(lines)
+    assert not bad, "\n".join(lines[max(0, i - 6): i + 1][-7:][0] + " ... " + lines[i] for i in bad[:5])
