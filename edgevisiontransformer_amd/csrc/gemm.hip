@@ -698,12 +698,12 @@ __device__ __forceinline__ void big8_stage(const P& p, char* smem, int wave, int
     if (j == 0 || j == 3) {
       const int row = (r & 63) + ((r >> 6) << 7) + (j == 3 ? 64 : 0);
       const int gm0 = min(m0 + row + srow, p.M - 1), gm1 = min(m0 + row + 8 + srow, p.M - 1);
-      glds16s_pair((const char*)p.A + (int64_t)m0 * (p.lda * 2) + Tg * ROWB - 1024,
+      glds16s_pair(((const char*)p.A - 1024 + (int64_t)m0 * (p.lda * 2)) + Tg * ROWB,
                    (uint32_t)((gm0 - m0) * (p.lda * 2)) + swz + 1024,
                    (uint32_t)((gm1 - m0) * (p.lda * 2)) + swz, base + row * ROWB);
     } else {
       const int row = ((r >> 5) << 6) + (r & 31) + (j == 2 ? 32 : 0);
-      glds16s_pair((const char*)p.W + (int64_t)n0 * (p.ldw * 2) + Tg * ROWB - 1024,
+      glds16s_pair(((const char*)p.W - 1024 + (int64_t)n0 * (p.ldw * 2)) + Tg * ROWB,
                    (uint32_t)((row + srow) * (p.ldw * 2)) + swz + 1024,
                    (uint32_t)((row + 8 + srow) * (p.ldw * 2)) + swz,
                    base + BIG_TILE + row * ROWB);
@@ -996,6 +996,14 @@ __device__ __forceinline__ void big8_loop(const P& p, char* smem,
     big8_kt<KT2, 0, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, false, 0, 0, {}, par, 0);
     mid();
     int t = 1;
+    // two K-tiles per iteration: t is odd in the first, even in the second, so each one's buffer
+    // parity (t ^ par) & 1 and region addresses are loop-invariant (round 6: SALU 42 -> 18.5 and
+    // VALU 6 -> 2 per K-tile; QKV 315.4 -> 310.9 µs, FC2 386.4 -> 377.7, DeiT-base +0.9 %,
+    // profiles/r06_unroll2_ab.txt)
+    for (; t + 3 < nk; t += 2) {
+      big8_kt<KT2, 0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, false, 0, 0, {}, par, 0);
+      big8_kt<KT2, 0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1, false, 0, 0, {}, par, 0);
+    }
     for (; t + 2 < nk; ++t)
       big8_kt<KT2, 0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, false, 0, 0, {}, par, 0);
     big8_kt<KT2, 1, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, cont, nm0, nn0, {}, par, npar);
