@@ -968,7 +968,7 @@ __device__ __forceinline__ void big8_kt(const P& p, char* smem,
 // K-tile's phase 3.
 template <int X, bool OPEN = false, typename Pre1 = NoOp, typename Mid = NoOp, int LX = 0,
           typename Last = NoOp, int LX3 = 0, typename Last3 = NoOp, typename P = GemmParams,
-          bool KT2 = false>
+          bool KT2 = false, bool U2 = false>
 __device__ __forceinline__ void big8_loop(const P& p, char* smem,
                                           f32x4 (&acc)[GeoOf<P>::NF][GeoOf<P>::MF],
                                           int wave, int lane, int wm, int wn, int m0, int n0,
@@ -996,13 +996,15 @@ __device__ __forceinline__ void big8_loop(const P& p, char* smem,
     big8_kt<KT2, 0, X>(p, smem, acc, wave, lane, wm, wn, m0, n0, 0, false, 0, 0, {}, par, 0);
     mid();
     int t = 1;
-    // two K-tiles per iteration: t is odd in the first, even in the second, so each one's buffer
-    // parity (t ^ par) & 1 and region addresses are loop-invariant (round 6: SALU 42 -> 18.5 and
-    // VALU 6 -> 2 per K-tile; QKV 315.4 -> 310.9 µs, FC2 386.4 -> 377.7, DeiT-base +0.9 %,
-    // profiles/r06_unroll2_ab.txt)
-    for (; t + 3 < nk; t += 2) {
-      big8_kt<KT2, 0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, false, 0, 0, {}, par, 0);
-      big8_kt<KT2, 0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1, false, 0, 0, {}, par, 0);
+    // U2: two K-tiles per iteration: t is odd in the first, even in the second, so each one's
+    // buffer parity (t ^ par) & 1 and region addresses are loop-invariant (round 6: SALU 42 -> 18.5
+    // and VALU 6 -> 2 per K-tile; QKV 315.4 -> 310.9 µs, FC2 386.4 -> 377.7, DeiT-base +0.9 %,
+    // profiles/r06_unroll2_ab.txt); not where the doubled body spills (pers_run)
+    if constexpr (U2) {
+      for (; t + 3 < nk; t += 2) {
+        big8_kt<KT2, 0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, false, 0, 0, {}, par, 0);
+        big8_kt<KT2, 0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t + 1, false, 0, 0, {}, par, 0);
+      }
     }
     for (; t + 2 < nk; ++t)
       big8_kt<KT2, 0, 0>(p, smem, acc, wave, lane, wm, wn, m0, n0, t, false, 0, 0, {}, par, 0);
@@ -1832,6 +1834,11 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
   // it no longer spills, measured equal to this rule: QKV 311.8 vs 311.9 us, r6c A/B)
   constexpr bool KT2 = (FL & EPI_LNIN) && (FL & (EPI_GELU | EPI_GELU_ERF)) &&
                        !(FL & (EPI_RESID | EPI_HM | EPI_STATS | EPI_GATHER | EPI_SPLIT));
+  // the two-K-tile steady loop (big8_loop U2) where its doubled body does not spill: not the
+  // gathered loaders (Swin PatchMerging, T2T soft splits), the Swin plain-residual epilogue or the
+  // column-padded (PADN) instances
+  constexpr bool U2 = !PADN && !(FL & (EPI_GATHER | EPI_SPLIT)) &&
+                      !((FL & EPI_RESID) && !(FL & EPI_RESLN));
   int tm, tn;
   pers_tile(tile, G, p.ntiles, xg, total, tm, tn);
   if (DBG == 5) {  // experiment: stagger the blocks' start
@@ -1887,14 +1894,14 @@ __device__ __forceinline__ void pers_run(const P& p, int total, int tile, char* 
                           ntn * BIG_BN, pre1, mid, {}, {}, par);
       else
         big8_loop<PERS_X, true, decltype(pre1), decltype(mid), (ER > 0 ? 4 : 0), decltype(last),
-                  (ER > 1 ? 4 : 0), decltype(last3), P, KT2>(
+                  (ER > 1 ? 4 : 0), decltype(last3), P, KT2, U2>(
             p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM, ntn * BIG_BN, pre1, mid,
             last, last3, par);
       stamp(1);
       if (has_next && !cont) big8_prologue(p, smem, wave, lane, ntm * BIG_BM, ntn * BIG_BN, nk);
     } else {
       big8_loop<PERS_X, false, NoOp, NoOp, (ER > 0 ? 4 : 0), decltype(last), (ER > 1 ? 4 : 0),
-                decltype(last3), P, KT2>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
+                decltype(last3), P, KT2, U2>(p, smem, acc, wave, ln, wm, wn, m0, n0, nk, cont, ntm * BIG_BM,
                                     ntn * BIG_BN, {}, {}, last, last3, par);
       stamp(1);
       pers_coef<FL>(p, smem, tid);
