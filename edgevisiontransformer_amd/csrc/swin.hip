@@ -620,7 +620,10 @@ __global__ __launch_bounds__(64 * MLP96_WAVES, 1) void swin_mlp96_kernel(SwinMlp
   __syncthreads();
   const float inv_d = 1.0f / (float)MLP96_C;
   const int ntiles = (p.M + 31) / 32;
-  for (int t = blockIdx.x * MLP96_WAVES + wave; t < ntiles; t += gridDim.x * MLP96_WAVES) {
+  // tile t of round k goes to wave (t mod W) / G of block t mod G (W = G waves x 12): the last,
+  // partial round spreads over every block (Swin-T bs256: 512 tiles past 8 full rounds = waves 0-1
+  // of all 256 blocks) instead of filling 43 blocks while the others idle
+  for (int t = wave * gridDim.x + blockIdx.x; t < ntiles; t += gridDim.x * MLP96_WAVES) {
     const int tok0 = t * 32;
     // B operand of FC1: LN2(xm) of token (16 tt + c16), k 32 ks + 8 g .. + 7, normalised in
     // registers ((x - mu) r; gamma is folded into W1, beta.W1 + b1 = cvec seeds the accumulator)
