@@ -504,8 +504,15 @@ thread_local int g_gemm_variant = 0;
 
 int num_cus();
 
+// The big kernels address inside a tile with 32-bit offsets: the LDS-DMA lane offsets (glds16s,
+// unsigned, up to 384 rows of lda / ldw) and the epilogue's buffer-descriptor ranges (signed, up
+// to 256 rows of ldc / ldr). Leading dimensions past that take the 128 x 128 kernel.
+constexpr int64_t BIG_MAX_LD = ((int64_t)1 << 31) / (2 * 384) - 64;
+
 bool use_big(const GemmParams& p, int flags) {
   if ((p.ntiles * GEMM_BN) % BIG_BN) return false;
+  if (std::max(std::max(p.lda, p.ldw), std::max(p.ldc, p.resid ? p.ldr : (int64_t)0)) > BIG_MAX_LD)
+    return false;
   if (!(flags & EPI_OUT_F32) && p.vec_ok < 2) return false;  // big epilogue: 16-B bf16 stores only
   // 31: automatic without 128 x 384, 36: automatic without grid balancing (launch_pers)
   const int v = (g_gemm_variant == 31 || g_gemm_variant == 36) ? 0 : g_gemm_variant;
@@ -2618,6 +2625,8 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
 bool use_p384(const GemmParams& p, int flags) {
   const int v = g_gemm_variant;
   if ((v != 0 && v != 30) || p.N % 384 || p.vec_ok < 2 || p.K < 64) return false;
+  if (std::max(std::max(p.lda, p.ldw), std::max(p.ldc, p.resid ? p.ldr : (int64_t)0)) > BIG_MAX_LD)
+    return false;
   if ((flags & (EPI_LNIN | EPI_RESLN)) && (p.nslots > 8 || p.nslots % 2 || p.stats_step > 1))
     return false;
   if ((flags & EPI_STATS) && 3 * (p.N / 384) > p.nslots) return false;

@@ -79,6 +79,44 @@ def _dense_case(gpu, dtype, M, K, N, flags):
     torch.testing.assert_close(got, ref, **tol)
 
 
+@pytest.mark.parametrize("variant", [0, 9])
+@pytest.mark.parametrize("resid", [False, True])
+def test_dense_huge_leading_dims(gpu, variant, resid):
+    """Leading dimensions past the big kernels' 32-bit in-tile offsets (gemm.hip BIG_MAX_LD:
+    ~2.8M elements; the LDS-DMA lane offsets wrap past 8.4M, the epilogue ranges past 4.2M) take
+    the 128 x 128 kernel, even under a forced persistent variant (9): A, C (and the residual)
+    rows 9M elements apart; bias + GELU into bf16, or bias + residual into fp32."""
+    M, K, N, LD = 300, 768, 768, 9_000_000
+    A64, W64 = _rand((M, K), 11), _rand((K, N), 12, scale=1.0 / math.sqrt(K))
+    b64, R64 = _rand((N,), 13, scale=0.1), _rand((M, N), 14)
+    A = torch.empty((M, LD), dtype=torch.bfloat16, device=gpu)
+    A[:, :K] = A64.to(torch.bfloat16).to(gpu)
+    wp, kpad, npad = _ops.pack(W64.float().to(gpu), "bf16")
+    bias = torch.zeros(npad, dtype=torch.float32, device=gpu)
+    bias[:N] = b64.float().to(gpu)
+    kw = {}
+    if resid:
+        flags = _lib.EPI_BIAS | _lib.EPI_RESID | _lib.EPI_OUT_F32
+        R = torch.empty((M, LD), dtype=torch.bfloat16, device=gpu)
+        R[:, :N] = R64.to(torch.bfloat16).to(gpu)
+        kw["resid"] = R
+        C = torch.zeros((M, LD), dtype=torch.float32, device=gpu)
+    else:
+        flags = _lib.EPI_BIAS | _lib.EPI_GELU
+        C = torch.zeros((M, LD), dtype=torch.bfloat16, device=gpu)
+    _lib.load_library().evt_set_gemm_variant(variant)
+    try:
+        _ops.dense("bf16", flags, A, wp, kpad, npad, M, N, ldc=LD, bias=bias, C=C, **kw)
+        torch.cuda.synchronize()
+    finally:
+        _lib.load_library().evt_set_gemm_variant(0)
+    ref = _q(A64, "bf16") @ _q(W64, "bf16") + b64
+    ref = ref + _q(R64, "bf16") if resid else _gelu(ref)
+    got = C[:, :N].double().cpu()
+    torch.testing.assert_close(got, ref, **(dict(rtol=1e-3, atol=1e-3) if resid else TOL["bf16"]))
+    assert not C[:, N:N + 64].any()  # nothing written past the N columns
+
+
 # only the valid (K, splits) pairs: the padded K must split into whole 64-deep K-tiles
 _SPLITK_SHAPES = [(M, K, N, s) for (M, K, N) in [(1, 768, 3072), (37, 3072, 1000), (130, 768, 148),
                                                   (257, 1536, 200)]
