@@ -108,6 +108,9 @@ SIGNATURES = {
     "evt_vit_forward": (_I, [_P, _P, _I, _P, _P]),
     "evt_query_workspace": (_I, [ctypes.POINTER(evt_vit_desc), _I, ctypes.POINTER(ctypes.c_size_t)]),
     "evt_model_destroy": (_I, [_P]),
+    "evt_model_set_lanes": (_I, [_P, _I, _P]),
+    "evt_model_lanes": (_I, [_P, ctypes.POINTER(_I)]),
+    "evt_model_set_lane_streams": (_I, [_P, _I, ctypes.POINTER(_P)]),
     "evt_graph_capture": (_I, [_P, _P, _I, _P, _P]),
     "evt_graph_launch": (_I, [_P, _P]),
     "evt_set_gemm_variant": (_I, [_I]),
@@ -201,3 +204,35 @@ def ensure_device(device_index: int) -> None:
 
 def stream_ptr(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
+
+
+# evt_model_set_lanes policy of the T2T-ViT / Swin mirrors: two lanes from 128 images (bf16).
+# Measured round 6 (scripts/stream_split_probe.py, one box, alternating): T2T-ViT-14 bs256
+# 58.0-58.2k -> 60.3-60.4k img/s, Swin-T bs256 57.5k -> 60.1-60.2k, logits bitwise equal; DeiT-base
+# bs512 28.6k vs 29.3k (ViT handles have no lanes).
+LANES_MIN_BATCH = 128
+
+
+def default_lanes(dtype: str, max_batch: int) -> int:
+    """Lane count for a new T2T-ViT / Swin handle; EVT_LANES=<k> overrides it (A/B runs)."""
+    env = os.environ.get("EVT_LANES", "")
+    if env:
+        return int(env)
+    return 2 if DTYPE[dtype] == DTYPE["bf16"] and max_batch >= LANES_MIN_BATCH else 1
+
+
+def set_lanes(handle: int, lanes: int, device) -> list:
+    """Give the handle `lanes` batch lanes on the streams the library creates, or with
+    EVT_LANE_STREAMS=torch on streams of torch's pool (evt_model_set_lane_streams; measured equal,
+    profiles/r06_lanes_probe.txt). Returns the torch streams (the model keeps them alive)."""
+    if lanes <= 1:
+        return []
+    lib = load_library()
+    check(lib.evt_model_set_lanes(ctypes.c_void_p(handle), lanes,
+                                  ctypes.c_void_p(stream_ptr(device))))
+    if os.environ.get("EVT_LANE_STREAMS", "") != "torch":
+        return []
+    streams = [torch.cuda.Stream(device) for _ in range(lanes)]
+    ptrs = (ctypes.c_void_p * lanes)(*[s.cuda_stream for s in streams])
+    check(lib.evt_model_set_lane_streams(ctypes.c_void_p(handle), lanes, ptrs))
+    return streams

@@ -171,6 +171,14 @@ struct evt_model {
   std::vector<int> prof_role;        // role of pair i of the last forward
   // algorithmic work of pair i (evt_model_profile_work): GFLOP and GB its kernels must do / move
   mutable std::vector<double> prof_gflop, prof_gbytes;
+  // evt_model_set_lanes: the batch split over k lanes, each a child model with its own workspace
+  // (the weights are this model's) on its own HIP stream, forked from / joined to the caller's
+  // stream by events; the kernels of the lanes then fill each other's idle CUs
+  std::vector<evt_model*> lanes;
+  std::vector<hipStream_t> lane_s;
+  std::vector<char> lane_own;        // lane_s[i] created (and destroyed) by the library
+  std::vector<hipEvent_t> lane_ev;   // [0]: fork, [1 + i]: lane i done
+  bool is_lane = false;              // a child: weights and lanes belong to the parent
 };
 
 namespace {
@@ -825,11 +833,24 @@ int evt_query_workspace(const evt_vit_desc* desc, int batch, size_t* bytes) {
   return EVT_OK;
 }
 
+// evt_model_set_lanes: the children (their workspaces), streams and events of a model
+static void release_lanes(evt_model* m) {
+  for (evt_model* c : m->lanes) evt_model_destroy(c);
+  for (size_t i = 0; i < m->lane_s.size(); ++i)
+    if (m->lane_own[i]) (void)hipStreamDestroy(m->lane_s[i]);
+  for (hipEvent_t e : m->lane_ev) (void)hipEventDestroy(e);
+  m->lanes.clear();
+  m->lane_s.clear();
+  m->lane_own.clear();
+  m->lane_ev.clear();
+}
+
 int evt_model_destroy(evt_model* m) {
   if (!m) return EVT_OK;
   // forwards enqueued on any stream may still read the workspace / weights: wait for the device
   // before freeing (hipFree would also synchronise, but only implicitly)
   (void)hipDeviceSynchronize();
+  release_lanes(m);
   if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
   if (m->graph) (void)hipGraphDestroy(m->graph);
   for (hipEvent_t e : m->prof_ev) (void)hipEventDestroy(e);
@@ -994,6 +1015,26 @@ int evt_t2t_query_workspace(const evt_t2t_desc* desc, int batch, size_t* bytes) 
   return EVT_OK;
 }
 
+// The T2T-ViT workspace for B images (activation buffers only; lanes allocate their own)
+static int t2t_alloc_ws(evt_model* m, int B, hipStream_t s) {
+  T2TShape ts;
+  EVT_RC(validate_t2t(&m->tdesc, &ts));
+  const size_t es = elem_size(m->dtype);
+  const size_t t1 = (size_t)B * ts.grid[0] * ts.grid[0];
+  EVT_RC(dev_alloc(m, &m->u, t2t_unfold_elems(ts, B) * es));
+  EVT_RC(dev_alloc(m, (void**)&m->su, t2t_unfold_stat_floats(ts, B) * sizeof(float)));
+  EVT_RC(dev_alloc(m, &m->kqvb, t1 * 3 * 64 * es));
+  EVT_RC(dev_alloc(m, &m->pout, t1 * 64 * es));
+  EVT_RC(dev_alloc(m, (void**)&m->tstats, t1 * 2 * sizeof(float)));
+  EVT_RC(dev_alloc(m, &m->zrow, 256));
+  EVT_HIP(hipMemsetAsync(m->zrow, 0, 256, s), "memset zero row");
+  EVT_RC(dev_alloc(m, (void**)&m->part, performer_part_floats(B, ts.grid[0] * ts.grid[0]) *
+                                            sizeof(float)));
+  EVT_RC(alloc_encoder_ws(m, B, (size_t)B * ts.enc.T * ts.enc.max_ffn_st * es, s));
+  m->ws_bytes = t2t_workspace_bytes(&m->tdesc, ts, B);
+  return EVT_OK;
+}
+
 int evt_t2t_create(const evt_t2t_desc* desc, const float* const* w, int n_weights, void* stream,
                    evt_model** out) {
   if (!out) return fail(EVT_EINVAL, "out is NULL");
@@ -1053,24 +1094,39 @@ int evt_t2t_create(const evt_t2t_desc* desc, const float* const* w, int n_weight
     k += 11 * desc->depth;
     // final LayerNorm (t2t_vit.py:111,129) folded into the classifier (:114,134)
     EVT_RC(make_dense(m, &m->head, w[k + 2], w[k + 3], D, desc->num_classes, s, w[k + 0], w[k + 1]));
-    const int B = desc->max_batch;
-    const size_t es = elem_size(desc->dtype);
-    const size_t t1 = (size_t)B * ts.grid[0] * ts.grid[0];
-    EVT_RC(dev_alloc(m, &m->u, t2t_unfold_elems(ts, B) * es));
-    EVT_RC(dev_alloc(m, (void**)&m->su, t2t_unfold_stat_floats(ts, B) * sizeof(float)));
-    EVT_RC(dev_alloc(m, &m->kqvb, t1 * 3 * 64 * es));
-    EVT_RC(dev_alloc(m, &m->pout, t1 * 64 * es));
-    EVT_RC(dev_alloc(m, (void**)&m->tstats, t1 * 2 * sizeof(float)));
-    EVT_RC(dev_alloc(m, &m->zrow, 256));
-    EVT_HIP(hipMemsetAsync(m->zrow, 0, 256, s), "memset zero row");
-    EVT_RC(dev_alloc(m, (void**)&m->part, performer_part_floats(B, ts.grid[0] * ts.grid[0]) *
-                                              sizeof(float)));
-    EVT_RC(alloc_encoder_ws(m, B, (size_t)B * ts.enc.T * ts.enc.max_ffn_st * es, s));
-    m->ws_bytes = t2t_workspace_bytes(desc, ts, B);
+    EVT_RC(t2t_alloc_ws(m, desc->max_batch, s));
     EVT_HIP(hipStreamSynchronize(s), "create sync");
     return EVT_OK;
   };
   return finish_create(m, run(), out);
+}
+
+static int swin_alloc_ws(evt_model* m, int B, hipStream_t s);  // (the Swin section)
+
+// A forward of B images over the model's lanes (evt_model_set_lanes): lane i takes images
+// [B i / k, B (i + 1) / k) on its own stream, forked from and joined to s by events (a HIP graph
+// capture on s records the lanes as parallel branches)
+typedef int (*ForwardFn)(evt_model*, const float*, int, float*, void*);
+static int lanes_forward(evt_model* m, ForwardFn fwd, const float* img, size_t img_elems, int B,
+                         float* logits, hipStream_t s) {
+  // the joins go onto s after every lane's work: a lane stream that shares s's hardware queue
+  // would otherwise queue its kernels behind s's wait for the previous lane (measured: lanes
+  // serialised in part)
+  const int k = (int)m->lanes.size();
+  EVT_HIP(hipEventRecord(m->lane_ev[0], s), "lanes fork");
+  for (int i = 0; i < k; ++i)
+    EVT_HIP(hipStreamWaitEvent(m->lane_s[i], m->lane_ev[0], 0), "lane fork wait");
+  for (int i = 0; i < k; ++i) {
+    const int b0 = (int)((int64_t)B * i / k), b1 = (int)((int64_t)B * (i + 1) / k);
+    if (b1 > b0)
+      EVT_RC(fwd(m->lanes[i], img + (size_t)b0 * img_elems, b1 - b0,
+                 logits + (size_t)b0 * m->num_classes, m->lane_s[i]));
+    EVT_HIP(hipEventRecord(m->lane_ev[1 + i], m->lane_s[i]), "lane done");
+  }
+  for (int i = 0; i < k; ++i)
+    EVT_HIP(hipStreamWaitEvent(s, m->lane_ev[1 + i], 0), "lanes join");
+  m->hm_layers = m->lanes[0]->hm_layers;
+  return EVT_OK;
 }
 
 int evt_t2t_forward(evt_model* m, const float* img, int B, float* logits, void* stream) {
@@ -1079,6 +1135,10 @@ int evt_t2t_forward(evt_model* m, const float* img, int B, float* logits, void* 
   if (B <= 0 || B > m->max_batch)
     return fail(EVT_EINVAL, "batch must be in [1, max_batch=" + std::to_string(m->max_batch) + "]");
   hipStream_t s = (hipStream_t)stream;
+  if (!m->lanes.empty() && !m->prof && B >= (int)m->lanes.size())  // profiling: one lane
+    return lanes_forward(m, evt_t2t_forward, img,
+                         (size_t)m->tdesc.image_size * m->tdesc.image_size * m->tdesc.in_chans, B,
+                         logits, s);
   prof_reset(m);
   const evt_t2t_desc& d = m->tdesc;
   const int dt = d.dtype, D = d.dim, T = m->sh.T, P = m->sh.P, S = d.image_size;
@@ -1247,6 +1307,87 @@ int evt_model_qkv_layout(const evt_model* m, int* headmajor_layers) {
   return EVT_OK;
 }
 
+int evt_model_set_lanes(evt_model* m, int lanes, void* stream) {
+  if (!m) return fail(EVT_EINVAL, "model is NULL");
+  if (m->is_lane) return fail(EVT_EINVAL, "the model is a lane of another model");
+  if (m->family == 0)
+    return fail(EVT_EINVAL, "lanes are for T2T-ViT and Swin models (ViT: measured slower)");
+  if (lanes < 1 || lanes > 4) return fail(EVT_EINVAL, "lanes must be in [1, 4]");
+  if (m->graph) return fail(EVT_EINVAL, "set the lanes before evt_graph_capture");
+  (void)hipDeviceSynchronize();  // forwards of the current lanes may still be running
+  release_lanes(m);
+  if (lanes == 1) return EVT_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int per = (m->max_batch + lanes - 1) / lanes;
+  auto run = [&]() -> int {
+    for (int i = 0; i < lanes; ++i) {
+      // the copy shares the parent's weights (its allocations stay the parent's); everything
+      // per-model is reset and the workspace allocated anew for `per` images
+      evt_model* c = new evt_model(*m);
+      c->allocs.clear();
+      c->lanes.clear();
+      c->lane_s.clear();
+      c->lane_own.clear();
+      c->lane_ev.clear();
+      c->graph = nullptr;
+      c->graph_exec = nullptr;
+      c->prof = false;
+      c->prof_ev.clear();
+      c->prof_role.clear();
+      c->prof_gflop.clear();
+      c->prof_gbytes.clear();
+      c->is_lane = true;
+      c->max_batch = per;
+      c->u = c->kqvb = c->pout = c->zrow = c->x = c->xm = c->qkv = c->o = c->hbuf = nullptr;
+      c->hh = c->sk = c->pooled = c->apatch = nullptr;
+      c->su = c->tstats = c->part = c->sx = c->sm = nullptr;
+      m->lanes.push_back(c);
+      EVT_RC(m->family == 1 ? t2t_alloc_ws(c, per, s) : swin_alloc_ws(c, per, s));
+      hipStream_t st = nullptr;
+      EVT_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "lane stream");
+      m->lane_s.push_back(st);
+      m->lane_own.push_back(1);
+    }
+    for (int i = 0; i <= lanes; ++i) {
+      hipEvent_t e = nullptr;
+      EVT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming), "lane event");
+      m->lane_ev.push_back(e);
+    }
+    EVT_HIP(hipStreamSynchronize(s), "lanes sync");
+    return EVT_OK;
+  };
+  const int rc = run();
+  if (rc) {
+    const std::string keep = g_err;
+    (void)hipDeviceSynchronize();
+    release_lanes(m);
+    g_err = keep;
+  }
+  return rc;
+}
+
+int evt_model_set_lane_streams(evt_model* m, int n, void* const* streams) {
+  if (!m || !streams) return fail(EVT_EINVAL, "null argument");
+  if (m->lanes.empty() || n != (int)m->lanes.size())
+    return fail(EVT_EINVAL, "n must equal the lane count (evt_model_set_lanes first)");
+  for (int i = 0; i < n; ++i)
+    if (!streams[i]) return fail(EVT_EINVAL, "lane streams must be non-NULL");
+  if (m->graph) return fail(EVT_EINVAL, "set the lane streams before evt_graph_capture");
+  (void)hipDeviceSynchronize();
+  for (int i = 0; i < n; ++i) {
+    if (m->lane_own[i]) (void)hipStreamDestroy(m->lane_s[i]);
+    m->lane_s[i] = (hipStream_t)streams[i];
+    m->lane_own[i] = 0;
+  }
+  return EVT_OK;
+}
+
+int evt_model_lanes(const evt_model* m, int* lanes) {
+  if (!m || !lanes) return fail(EVT_EINVAL, "null argument");
+  *lanes = m->lanes.empty() ? 1 : (int)m->lanes.size();
+  return EVT_OK;
+}
+
 int evt_model_profile_work(evt_model* m, double* gflop, double* gbytes) {
   if (!m || !gflop || !gbytes) return fail(EVT_EINVAL, "null argument");
   for (int r = 0; r < EVT_PROF_ROLES; ++r) gflop[r] = gbytes[r] = 0.0;
@@ -1316,6 +1457,31 @@ int evt_swin_query_workspace(const evt_swin_desc* desc, int batch, size_t* bytes
   return EVT_OK;
 }
 
+// The Swin workspace for B images (activation buffers only; lanes allocate their own)
+static int swin_alloc_ws(evt_model* m, int B, hipStream_t s) {
+  SwinGeo g;
+  EVT_RC(validate_swin(&m->sdesc, &g));
+  const SwinWs ws = swin_ws(g, B);
+  const size_t es = elem_size(m->dtype);
+  EVT_RC(dev_alloc(m, &m->x, (ws.stream + SWIN_SLACK) * es));
+  EVT_RC(dev_alloc(m, &m->xm, (ws.stream + SWIN_SLACK) * es));
+  EVT_HIP(hipMemsetAsync(m->x, 0, (ws.stream + SWIN_SLACK) * es, s), "memset x");
+  EVT_HIP(hipMemsetAsync(m->xm, 0, (ws.stream + SWIN_SLACK) * es, s), "memset xm");
+  EVT_RC(dev_alloc(m, (void**)&m->sx, ws.stats * sizeof(float)));
+  EVT_RC(dev_alloc(m, (void**)&m->sm, ws.stats * sizeof(float)));
+  EVT_RC(dev_alloc(m, &m->qkv, ws.qkv * es));
+  EVT_RC(dev_alloc(m, &m->o, (ws.o + SWIN_SLACK) * es));
+  EVT_HIP(hipMemsetAsync(m->o, 0, (ws.o + SWIN_SLACK) * es, s), "memset o");
+  EVT_RC(dev_alloc(m, &m->hbuf, ws.hbuf * es));
+  EVT_RC(dev_alloc(m, &m->pooled, ws.pooled * es));
+  if (m->dtype == DT_BF16) {
+    EVT_RC(dev_alloc(m, &m->sk, gemm_sk_bytes()));
+    EVT_HIP(hipMemsetAsync(m->sk, 0, 4096, s), "memset stream-K flags");
+  }
+  m->ws_bytes = swin_workspace_bytes(&m->sdesc, g, B);
+  return EVT_OK;
+}
+
 int evt_swin_create(const evt_swin_desc* desc, const float* const* w, int n_weights, void* stream,
                     evt_model** out) {
   if (!out) return fail(EVT_EINVAL, "out is NULL");
@@ -1372,25 +1538,7 @@ int evt_swin_create(const evt_swin_desc* desc, const float* const* w, int n_weig
     EVT_RC(copy_vec(m, &m->norm_g, w[k + 0], nf, s));
     EVT_RC(copy_vec(m, &m->norm_b, w[k + 1], nf, s));
     EVT_RC(make_dense(m, &m->head, w[k + 2], w[k + 3], nf, desc->num_classes, s));
-    const int B = desc->max_batch;
-    const SwinWs ws = swin_ws(g, B);
-    const size_t es = elem_size(desc->dtype);
-    EVT_RC(dev_alloc(m, &m->x, (ws.stream + SWIN_SLACK) * es));
-    EVT_RC(dev_alloc(m, &m->xm, (ws.stream + SWIN_SLACK) * es));
-    EVT_HIP(hipMemsetAsync(m->x, 0, (ws.stream + SWIN_SLACK) * es, s), "memset x");
-    EVT_HIP(hipMemsetAsync(m->xm, 0, (ws.stream + SWIN_SLACK) * es, s), "memset xm");
-    EVT_RC(dev_alloc(m, (void**)&m->sx, ws.stats * sizeof(float)));
-    EVT_RC(dev_alloc(m, (void**)&m->sm, ws.stats * sizeof(float)));
-    EVT_RC(dev_alloc(m, &m->qkv, ws.qkv * es));
-    EVT_RC(dev_alloc(m, &m->o, (ws.o + SWIN_SLACK) * es));
-    EVT_HIP(hipMemsetAsync(m->o, 0, (ws.o + SWIN_SLACK) * es, s), "memset o");
-    EVT_RC(dev_alloc(m, &m->hbuf, ws.hbuf * es));
-    EVT_RC(dev_alloc(m, &m->pooled, ws.pooled * es));
-    if (desc->dtype == DT_BF16) {
-      EVT_RC(dev_alloc(m, &m->sk, gemm_sk_bytes()));
-      EVT_HIP(hipMemsetAsync(m->sk, 0, 4096, s), "memset stream-K flags");
-    }
-    m->ws_bytes = swin_workspace_bytes(desc, g, B);
+    EVT_RC(swin_alloc_ws(m, desc->max_batch, s));
     EVT_HIP(hipStreamSynchronize(s), "create sync");
     return EVT_OK;
   };
@@ -1403,6 +1551,10 @@ int evt_swin_forward(evt_model* m, const float* img, int B, float* logits, void*
   if (B <= 0 || B > m->max_batch)
     return fail(EVT_EINVAL, "batch must be in [1, max_batch=" + std::to_string(m->max_batch) + "]");
   hipStream_t s = (hipStream_t)stream;
+  if (!m->lanes.empty() && !m->prof && B >= (int)m->lanes.size())  // profiling: one lane
+    return lanes_forward(m, evt_swin_forward, img,
+                         (size_t)m->sdesc.in_chans * m->sdesc.image_size * m->sdesc.image_size, B,
+                         logits, s);
   prof_reset(m);
   const evt_swin_desc& d = m->sdesc;
   const int dt = d.dtype;

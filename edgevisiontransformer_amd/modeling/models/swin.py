@@ -41,7 +41,7 @@ class SwinTransformer:
                  qkv_bias=True, qk_scale=None, drop_rate=0., drop_path_rate=0.1, ape=False,
                  patch_norm=True, use_checkpoint=False, *, dtype: str = "bf16", seed: int = 0,
                  weights: Optional[Dict[str, np.ndarray]] = None, device=None,
-                 max_batch: int = 0):
+                 max_batch: int = 0, lanes: Optional[int] = None):
         if window_size != 7:
             raise ValueError("window_size must be 7 in this build")
         if ape or not patch_norm or not qkv_bias or qk_scale is not None:
@@ -76,6 +76,8 @@ class SwinTransformer:
             self._weights.append(torch.from_numpy(np.ascontiguousarray(a)).to(self.device))
         self._handle: Optional[int] = None
         self._max_batch = 0
+        # batch lanes (evt_model_set_lanes): None = _lib.default_lanes
+        self._lanes = lanes
         if max_batch:
             self._build(max_batch)
 
@@ -108,6 +110,17 @@ class SwinTransformer:
                                            ctypes.byref(out)))
         self._handle = out.value
         self._max_batch = max_batch
+        with torch.cuda.device(self.device):
+            self._lane_streams = _lib.set_lanes(
+                self._handle, self._lanes if self._lanes is not None
+                else _lib.default_lanes(self.dtype, max_batch), self.device)
+
+    def lanes(self) -> int:
+        """Batch lanes of the handle (include/evt.h evt_model_set_lanes; 1 = none)."""
+        out = ctypes.c_int()
+        _lib.check(_lib.load_library().evt_model_lanes(ctypes.c_void_p(self._handle),
+                                                       ctypes.byref(out)))
+        return out.value
 
     def workspace_bytes(self, batch: int) -> int:
         out = ctypes.c_size_t()

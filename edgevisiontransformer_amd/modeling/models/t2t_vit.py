@@ -36,7 +36,7 @@ class T2T_ViT:
                  qkv_bias=False, qk_scale=None, drop_rate=0., attn_drop_rate=0.,
                  drop_path_rate=0., *, dtype: str = "bf16", seed: int = 0,
                  weights: Optional[Dict[str, np.ndarray]] = None, device=None,
-                 max_batch: int = 0):
+                 max_batch: int = 0, lanes: Optional[int] = None):
         if tokens_type != "performer":  # t2t_vit.py:58-59
             raise NotImplementedError(
                 "T2T_module with token_type other than performer is not supported")
@@ -64,6 +64,8 @@ class T2T_ViT:
                                  .to(self.device))
         self._handle: Optional[int] = None
         self._max_batch = 0
+        # batch lanes (evt_model_set_lanes): None = _lib.default_lanes
+        self._lanes = lanes
         if max_batch:
             self._build(max_batch)
 
@@ -86,6 +88,17 @@ class T2T_ViT:
                                           ctypes.byref(out)))
         self._handle = out.value
         self._max_batch = max_batch
+        with torch.cuda.device(self.device):
+            self._lane_streams = _lib.set_lanes(
+                self._handle, self._lanes if self._lanes is not None
+                else _lib.default_lanes(self.dtype, max_batch), self.device)
+
+    def lanes(self) -> int:
+        """Batch lanes of the handle (include/evt.h evt_model_set_lanes; 1 = none)."""
+        out = ctypes.c_int()
+        _lib.check(_lib.load_library().evt_model_lanes(ctypes.c_void_p(self._handle),
+                                                       ctypes.byref(out)))
+        return out.value
 
     def workspace_bytes(self, batch: int) -> int:
         lib = _lib.load_library()

@@ -118,6 +118,28 @@ int evt_query_workspace(const evt_vit_desc* desc, int batch, size_t* bytes);
  * any stream finish first). NULL is accepted. */
 int evt_model_destroy(evt_model* model);
 
+/* Batch lanes (T2T-ViT and Swin handles; the reference's tools.py times one model.call per batch,
+ * tools.py:82-116): with lanes = k > 1 every later forward of batch >= k splits its images into k
+ * contiguous parts of sizes differing by at most one, each run by a child of the handle (the
+ * handle's weights, its own workspace for ceil(max_batch / k) images: about k + 1 workspaces in
+ * all) on its own HIP stream, forked from and joined to the caller's stream by events, so the
+ * kernels of the parts fill each other's idle CUs (the GEMMs at 1.5 tile rounds, the latency-bound
+ * fused Swin stage-1 kernels). Logits are the same as the one-lane forward's wherever the parts
+ * take the same kernels as the whole batch (bitwise at the BASELINE batch sizes, tests/
+ * test_gpu_lanes.py). Forwards while profiling (evt_model_profile) run as one lane. lanes = 1
+ * drops the children. Synchronises the device; call before evt_graph_capture (a capture records
+ * the lanes as parallel branches). `stream` orders the workspace initialisation. EVT_EINVAL for
+ * ViT handles (measured slower at DeiT-base bs512: DESIGN.md) and lanes outside [1, 4]. */
+int evt_model_set_lanes(evt_model* model, int lanes, void* stream);
+/* Run the lanes on the caller's streams (n = the lane count; they must outlive the handle or
+ * the next evt_model_set_lanes) instead of the ones evt_model_set_lanes created (destroyed here):
+ * for a host framework's stream pool. Each lane stream should map to its own hardware queue, apart
+ * from the other lanes' (HIP gives a new stream the least-used of GPU_MAX_HW_QUEUES queues; two
+ * lanes on one queue run one after the other). Synchronises the device. */
+int evt_model_set_lane_streams(evt_model* model, int n, void* const* streams);
+/* The handle's lane count (1 without lanes). */
+int evt_model_lanes(const evt_model* model, int* lanes);
+
 /* ---- op-level entry points (one per hot-path kernel; used by the parity tests) ---------- */
 
 

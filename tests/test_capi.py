@@ -27,7 +27,7 @@ def lib():
 def test_header_and_binding_agree():
     from edgevisiontransformer_amd import _lib
     assert _declared() == sorted(_lib.SIGNATURES)
-    assert len(_declared()) == 41
+    assert len(_declared()) == 44
 
 
 def test_every_declared_symbol_is_exported(lib):

@@ -94,3 +94,18 @@ def test_t2t_rejects_unsupported_tokens_type():
     from edgevisiontransformer_amd.modeling.models.t2t_vit import T2T_ViT
     with pytest.raises(NotImplementedError):
         T2T_ViT(tokens_type="transformer")
+
+
+def test_default_lanes_policy(monkeypatch):
+    """Batch lanes of new T2T-ViT / Swin handles (_lib.default_lanes): two from 128 images in
+    bf16, one otherwise; EVT_LANES overrides (the A/B switch)."""
+    from edgevisiontransformer_amd import _lib
+    monkeypatch.delenv("EVT_LANES", raising=False)
+    assert _lib.default_lanes("bf16", 256) == 2
+    assert _lib.default_lanes("bf16", _lib.LANES_MIN_BATCH) == 2
+    assert _lib.default_lanes("bf16", _lib.LANES_MIN_BATCH - 1) == 1
+    assert _lib.default_lanes("f32", 256) == 1
+    monkeypatch.setenv("EVT_LANES", "1")
+    assert _lib.default_lanes("bf16", 256) == 1
+    monkeypatch.setenv("EVT_LANES", "3")
+    assert _lib.default_lanes("f32", 8) == 3
