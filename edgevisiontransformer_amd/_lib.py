@@ -206,19 +206,22 @@ def stream_ptr(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
-# evt_model_set_lanes policy of the T2T-ViT / Swin mirrors: two lanes from 128 images (bf16).
-# Measured round 6 (scripts/stream_split_probe.py, one box, alternating): T2T-ViT-14 bs256
-# 58.0-58.2k -> 60.3-60.4k img/s, Swin-T bs256 57.5k -> 60.1-60.2k, logits bitwise equal; DeiT-base
-# bs512 28.6k vs 29.3k (ViT handles have no lanes).
+# evt_model_set_lanes policy of the mirrors: two lanes from 128 images for T2T-ViT / Swin in bf16
+# and for ViT in fp32. Measured round 6 (bench.py A/B on one box per call, profiles/
+# r06_lanes_ab.txt): T2T-ViT-14 bs256 +0.7-1.8 %, Swin-T bs256 +0.5-3.3 %, DeiT-tiny fp32 bs256
+# +19 %, logits bitwise equal; bf16 ViT stays one lane (DeiT-base bs512 / bs64 slower split).
 LANES_MIN_BATCH = 128
 
 
-def default_lanes(dtype: str, max_batch: int) -> int:
-    """Lane count for a new T2T-ViT / Swin handle; EVT_LANES=<k> overrides it (A/B runs)."""
+def default_lanes(dtype: str, max_batch: int, vit: bool = False) -> int:
+    """Lane count for a new handle; EVT_LANES=<k> overrides it (A/B runs)."""
     env = os.environ.get("EVT_LANES", "")
     if env:
         return int(env)
-    return 2 if DTYPE[dtype] == DTYPE["bf16"] and max_batch >= LANES_MIN_BATCH else 1
+    if max_batch < LANES_MIN_BATCH:
+        return 1
+    want = DTYPE["f32"] if vit else DTYPE["bf16"]
+    return 2 if DTYPE[dtype] == want else 1
 
 
 def set_lanes(handle: int, lanes: int, device) -> list:

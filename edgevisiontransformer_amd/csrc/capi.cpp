@@ -859,6 +859,65 @@ int evt_model_destroy(evt_model* m) {
   return EVT_OK;
 }
 
+static int swin_alloc_ws(evt_model* m, int B, hipStream_t s);  // (the Swin section)
+
+// A forward of B images over the model's lanes (evt_model_set_lanes): lane i takes images
+// [B i / k, B (i + 1) / k) on its own stream, forked from and joined to s by events (a HIP graph
+// capture on s records the lanes as parallel branches)
+typedef int (*ForwardFn)(evt_model*, const float*, int, float*, void*);
+static int lanes_forward(evt_model* m, ForwardFn fwd, const float* img, size_t img_elems, int B,
+                         float* logits, hipStream_t s) {
+  // the joins go onto s after every lane's work: a lane stream that shares s's hardware queue
+  // would otherwise queue its kernels behind s's wait for the previous lane (measured: lanes
+  // serialised in part)
+  const int k = (int)m->lanes.size();
+  EVT_HIP(hipEventRecord(m->lane_ev[0], s), "lanes fork");
+  for (int i = 0; i < k; ++i)
+    EVT_HIP(hipStreamWaitEvent(m->lane_s[i], m->lane_ev[0], 0), "lane fork wait");
+  for (int i = 0; i < k; ++i) {
+    const int b0 = (int)((int64_t)B * i / k), b1 = (int)((int64_t)B * (i + 1) / k);
+    if (b1 > b0)
+      EVT_RC(fwd(m->lanes[i], img + (size_t)b0 * img_elems, b1 - b0,
+                 logits + (size_t)b0 * m->num_classes, m->lane_s[i]));
+    EVT_HIP(hipEventRecord(m->lane_ev[1 + i], m->lane_s[i]), "lane done");
+  }
+  for (int i = 0; i < k; ++i)
+    EVT_HIP(hipStreamWaitEvent(s, m->lane_ev[1 + i], 0), "lanes join");
+  m->hm_layers = m->lanes[0]->hm_layers;
+  return EVT_OK;
+}
+
+// The ViT workspace for B images (activation buffers only; lanes allocate their own)
+static int vit_alloc_ws(evt_model* m, int B, hipStream_t s) {
+  const Shape& sh = m->sh;
+  const int D = m->D;
+  const size_t es = elem_size(m->dtype);
+  EVT_RC(alloc_encoder_ws(m, B, std::max((size_t)B * sh.T * sh.max_ffn_st,
+                                         (size_t)B * sh.P * sh.pd) * es, s));
+  m->apatch = m->hbuf;
+  EVT_RC(dev_alloc(m, &m->hh, (size_t)B * sh.head_st * es));
+  if (m->mx8) {
+    const size_t rows = (size_t)B * sh.T;
+    m->qa_ld = (int)std::max(round_up(D, 128), round_up(sh.max_inner, 128));
+    int maxffn = 0;
+    for (int f : m->ffn) maxffn = std::max(maxffn, f);
+    m->qh_ld = (int)round_up(maxffn, 128);
+    EVT_RC(dev_alloc(m, &m->qa, rows * m->qa_ld));
+    EVT_RC(dev_alloc(m, (void**)&m->sa, rows * (m->qa_ld / 128) * 4));
+    EVT_RC(dev_alloc(m, &m->qh, rows * m->qh_ld));
+    EVT_RC(dev_alloc(m, (void**)&m->shd, rows * (m->qh_ld / 128) * 4));
+    EVT_RC(dev_alloc(m, (void**)&m->lnst, rows * 2 * sizeof(float)));
+    // every byte of the MX8 operands is written finite before it is read (NaN-free padding)
+    EVT_HIP(hipMemsetAsync(m->qa, 0, rows * m->qa_ld, s), "memset qa");
+    EVT_HIP(hipMemsetAsync(m->sa, 0, rows * (m->qa_ld / 128) * 4, s), "memset qa scales");
+    // FC1 writes columns < roundup(ffn, 32) only: the rest of the FC2 operand stays zero
+    EVT_HIP(hipMemsetAsync(m->qh, 0, rows * m->qh_ld, s), "memset qh");
+    EVT_HIP(hipMemsetAsync(m->shd, 0, rows * (m->qh_ld / 128) * 4, s), "memset qh scales");
+  }
+  m->ws_bytes = workspace_bytes(&m->desc, sh, B);
+  return EVT_OK;
+}
+
 int evt_vit_create(const evt_vit_desc* desc, const float* const* w, int n_weights, void* stream,
                    evt_model** out) {
   if (!out) return fail(EVT_EINVAL, "out is NULL");
@@ -913,31 +972,7 @@ int evt_vit_create(const evt_vit_desc* desc, const float* const* w, int n_weight
       EVT_RC(make_dense(m, &m->head1, w[k + 0], w[k + 1], D, desc->mlp_dim, s));
       EVT_RC(make_dense(m, &m->head2, w[k + 2], w[k + 3], desc->mlp_dim, desc->num_classes, s));
     }
-    const int B = desc->max_batch;
-    const size_t es = elem_size(m->dtype);
-    EVT_RC(alloc_encoder_ws(m, B, std::max((size_t)B * sh.T * sh.max_ffn_st,
-                                           (size_t)B * sh.P * sh.pd) * es, s));
-    m->apatch = m->hbuf;
-    EVT_RC(dev_alloc(m, &m->hh, (size_t)B * sh.head_st * es));
-    if (m->mx8) {
-      const size_t rows = (size_t)B * sh.T;
-      m->qa_ld = (int)std::max(round_up(D, 128), round_up(sh.max_inner, 128));
-      int maxffn = 0;
-      for (int f : m->ffn) maxffn = std::max(maxffn, f);
-      m->qh_ld = (int)round_up(maxffn, 128);
-      EVT_RC(dev_alloc(m, &m->qa, rows * m->qa_ld));
-      EVT_RC(dev_alloc(m, (void**)&m->sa, rows * (m->qa_ld / 128) * 4));
-      EVT_RC(dev_alloc(m, &m->qh, rows * m->qh_ld));
-      EVT_RC(dev_alloc(m, (void**)&m->shd, rows * (m->qh_ld / 128) * 4));
-      EVT_RC(dev_alloc(m, (void**)&m->lnst, rows * 2 * sizeof(float)));
-      // every byte of the MX8 operands is written finite before it is read (NaN-free padding)
-      EVT_HIP(hipMemsetAsync(m->qa, 0, rows * m->qa_ld, s), "memset qa");
-      EVT_HIP(hipMemsetAsync(m->sa, 0, rows * (m->qa_ld / 128) * 4, s), "memset qa scales");
-      // FC1 writes columns < roundup(ffn, 32) only: the rest of the FC2 operand stays zero
-      EVT_HIP(hipMemsetAsync(m->qh, 0, rows * m->qh_ld, s), "memset qh");
-      EVT_HIP(hipMemsetAsync(m->shd, 0, rows * (m->qh_ld / 128) * 4, s), "memset qh scales");
-    }
-    m->ws_bytes = workspace_bytes(desc, sh, B);
+    EVT_RC(vit_alloc_ws(m, desc->max_batch, s));
     EVT_HIP(hipStreamSynchronize(s), "create sync");
     return EVT_OK;
   };
@@ -950,6 +985,10 @@ int evt_vit_forward(evt_model* m, const float* img, int B, float* logits, void* 
   if (B <= 0 || B > m->max_batch)
     return fail(EVT_EINVAL, "batch must be in [1, max_batch=" + std::to_string(m->max_batch) + "]");
   hipStream_t s = (hipStream_t)stream;
+  if (!m->lanes.empty() && !m->prof && B >= (int)m->lanes.size())  // profiling: one lane
+    return lanes_forward(m, evt_vit_forward, img,
+                         (size_t)m->desc.in_chans * m->desc.image_size * m->desc.image_size, B,
+                         logits, s);
   const evt_vit_desc& d = m->desc;
   const Shape& sh = m->sh;
   const int D = d.dim, T = sh.T, dt = m->dtype;
@@ -1099,34 +1138,6 @@ int evt_t2t_create(const evt_t2t_desc* desc, const float* const* w, int n_weight
     return EVT_OK;
   };
   return finish_create(m, run(), out);
-}
-
-static int swin_alloc_ws(evt_model* m, int B, hipStream_t s);  // (the Swin section)
-
-// A forward of B images over the model's lanes (evt_model_set_lanes): lane i takes images
-// [B i / k, B (i + 1) / k) on its own stream, forked from and joined to s by events (a HIP graph
-// capture on s records the lanes as parallel branches)
-typedef int (*ForwardFn)(evt_model*, const float*, int, float*, void*);
-static int lanes_forward(evt_model* m, ForwardFn fwd, const float* img, size_t img_elems, int B,
-                         float* logits, hipStream_t s) {
-  // the joins go onto s after every lane's work: a lane stream that shares s's hardware queue
-  // would otherwise queue its kernels behind s's wait for the previous lane (measured: lanes
-  // serialised in part)
-  const int k = (int)m->lanes.size();
-  EVT_HIP(hipEventRecord(m->lane_ev[0], s), "lanes fork");
-  for (int i = 0; i < k; ++i)
-    EVT_HIP(hipStreamWaitEvent(m->lane_s[i], m->lane_ev[0], 0), "lane fork wait");
-  for (int i = 0; i < k; ++i) {
-    const int b0 = (int)((int64_t)B * i / k), b1 = (int)((int64_t)B * (i + 1) / k);
-    if (b1 > b0)
-      EVT_RC(fwd(m->lanes[i], img + (size_t)b0 * img_elems, b1 - b0,
-                 logits + (size_t)b0 * m->num_classes, m->lane_s[i]));
-    EVT_HIP(hipEventRecord(m->lane_ev[1 + i], m->lane_s[i]), "lane done");
-  }
-  for (int i = 0; i < k; ++i)
-    EVT_HIP(hipStreamWaitEvent(s, m->lane_ev[1 + i], 0), "lanes join");
-  m->hm_layers = m->lanes[0]->hm_layers;
-  return EVT_OK;
 }
 
 int evt_t2t_forward(evt_model* m, const float* img, int B, float* logits, void* stream) {
@@ -1310,8 +1321,6 @@ int evt_model_qkv_layout(const evt_model* m, int* headmajor_layers) {
 int evt_model_set_lanes(evt_model* m, int lanes, void* stream) {
   if (!m) return fail(EVT_EINVAL, "model is NULL");
   if (m->is_lane) return fail(EVT_EINVAL, "the model is a lane of another model");
-  if (m->family == 0)
-    return fail(EVT_EINVAL, "lanes are for T2T-ViT and Swin models (ViT: measured slower)");
   if (lanes < 1 || lanes > 4) return fail(EVT_EINVAL, "lanes must be in [1, 4]");
   if (m->graph) return fail(EVT_EINVAL, "set the lanes before evt_graph_capture");
   (void)hipDeviceSynchronize();  // forwards of the current lanes may still be running
@@ -1339,10 +1348,13 @@ int evt_model_set_lanes(evt_model* m, int lanes, void* stream) {
       c->is_lane = true;
       c->max_batch = per;
       c->u = c->kqvb = c->pout = c->zrow = c->x = c->xm = c->qkv = c->o = c->hbuf = nullptr;
-      c->hh = c->sk = c->pooled = c->apatch = nullptr;
-      c->su = c->tstats = c->part = c->sx = c->sm = nullptr;
+      c->hh = c->sk = c->pooled = c->apatch = c->qa = c->qh = nullptr;
+      c->su = c->tstats = c->part = c->sx = c->sm = c->lnst = nullptr;
+      c->sa = c->shd = nullptr;
       m->lanes.push_back(c);
-      EVT_RC(m->family == 1 ? t2t_alloc_ws(c, per, s) : swin_alloc_ws(c, per, s));
+      EVT_RC(m->family == 0   ? vit_alloc_ws(c, per, s)
+             : m->family == 1 ? t2t_alloc_ws(c, per, s)
+                              : swin_alloc_ws(c, per, s));
       hipStream_t st = nullptr;
       EVT_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "lane stream");
       m->lane_s.push_back(st);

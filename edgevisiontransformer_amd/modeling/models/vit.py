@@ -99,7 +99,7 @@ class ViT:
     def __init__(self, *, image_size=224, patch_size=16, num_classes=1000, dim=768, depth=12,
                  heads=12, mlp_dim=3072, dtype: str = "bf16", seed: int = 0,
                  weights: Optional[Dict[str, np.ndarray]] = None, device=None, max_batch: int = 0,
-                 _cfg: Optional[ViTConfig] = None):
+                 lanes: Optional[int] = None, _cfg: Optional[ViTConfig] = None):
         assert image_size % patch_size == 0, "image dimensions must be divisible by the patch size"
         if _cfg is None:
             if dim % heads != 0:  # reference Attention raises ValueError (attention.py:8-9)
@@ -128,6 +128,8 @@ class ViT:
         self._handle: Optional[int] = None
         self._max_batch = 0
         self._arrays = None
+        # batch lanes (evt_model_set_lanes): None = _lib.default_lanes
+        self._lanes = lanes
         if max_batch:
             self._build(max_batch)
 
@@ -155,6 +157,17 @@ class ViT:
                                           ctypes.byref(out)))
         self._handle = out.value
         self._max_batch = max_batch
+        with torch.cuda.device(self.device):
+            self._lane_streams = _lib.set_lanes(
+                self._handle, self._lanes if self._lanes is not None
+                else _lib.default_lanes(self.dtype, max_batch, vit=True), self.device)
+
+    def lanes(self) -> int:
+        """Batch lanes of the handle (include/evt.h evt_model_set_lanes; 1 = none)."""
+        out = ctypes.c_int()
+        _lib.check(_lib.load_library().evt_model_lanes(ctypes.c_void_p(self._handle),
+                                                       ctypes.byref(out)))
+        return out.value
 
     def qkv_headmajor_layers(self) -> int:
         """Encoder layers whose QKV output was stored head-major in the last forward

@@ -118,7 +118,7 @@ int evt_query_workspace(const evt_vit_desc* desc, int batch, size_t* bytes);
  * any stream finish first). NULL is accepted. */
 int evt_model_destroy(evt_model* model);
 
-/* Batch lanes (T2T-ViT and Swin handles; the reference's tools.py times one model.call per batch,
+/* Batch lanes (any handle; the reference's tools.py times one model.call per batch,
  * tools.py:82-116): with lanes = k > 1 every later forward of batch >= k splits its images into k
  * contiguous parts of sizes differing by at most one, each run by a child of the handle (the
  * handle's weights, its own workspace for ceil(max_batch / k) images: about k + 1 workspaces in
@@ -129,7 +129,8 @@ int evt_model_destroy(evt_model* model);
  * test_gpu_lanes.py). Forwards while profiling (evt_model_profile) run as one lane. lanes = 1
  * drops the children. Synchronises the device; call before evt_graph_capture (a capture records
  * the lanes as parallel branches). `stream` orders the workspace initialisation. EVT_EINVAL for
- * ViT handles (measured slower at DeiT-base bs512: DESIGN.md) and lanes outside [1, 4]. */
+ * lanes outside [1, 4]. Measured: faster for T2T-ViT-14 / Swin-T bf16 and DeiT-tiny
+ * fp32 at 256 images, slower for DeiT-base bf16 (512 and 64 images) and DeiT-tiny bf16. */
 int evt_model_set_lanes(evt_model* model, int lanes, void* stream);
 /* Run the lanes on the caller's streams (n = the lane count; they must outlive the handle or
  * the next evt_model_set_lanes) instead of the ones evt_model_set_lanes created (destroyed here):

@@ -13,6 +13,7 @@ from edgevisiontransformer_amd.modeling.models import swin, t2t_vit, vit  # noqa
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 MODEL = sys.argv[2] if len(sys.argv) > 2 else "deit_base"
 MOD = swin if MODEL.startswith("swin") else t2t_vit if MODEL.startswith("t2t") else vit
+DTYPE = __import__("os").environ.get("PROBE_DTYPE", "bf16")
 SHAPE = (224, 224, 3) if MODEL.startswith("t2t") else (3, 224, 224)  # T2T-ViT is channel-last
 dev = torch.device("cuda", 0)
 g = torch.Generator(device="cuda").manual_seed(1000)
@@ -40,7 +41,7 @@ def arm(k, steps=50, warm=5, lanes=1, raw=False, cumask=False, libstreams=False)
     import os
     kw = {"lanes": lanes} if MOD is not vit else {}
     os.environ["EVT_LANE_STREAMS"] = "" if libstreams else "torch"
-    models = [MOD.build_named(MODEL, dtype="bf16", seed=0, max_batch=B // k, **kw) for _ in range(k)]
+    models = [MOD.build_named(MODEL, dtype=DTYPE, seed=0, max_batch=B // k, **kw) for _ in range(k)]
     os.environ["EVT_LANE_STREAMS"] = ""
     streams = [_raw_stream(cumask) if raw else torch.cuda.Stream() for _ in range(k)]
     outs = [torch.empty((B // k, 1000), device="cuda") for _ in range(k)]

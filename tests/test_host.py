@@ -105,6 +105,9 @@ def test_default_lanes_policy(monkeypatch):
     assert _lib.default_lanes("bf16", _lib.LANES_MIN_BATCH) == 2
     assert _lib.default_lanes("bf16", _lib.LANES_MIN_BATCH - 1) == 1
     assert _lib.default_lanes("f32", 256) == 1
+    assert _lib.default_lanes("f32", 256, vit=True) == 2   # ViT: the fp32 path
+    assert _lib.default_lanes("bf16", 512, vit=True) == 1
+    assert _lib.default_lanes("f32", 64, vit=True) == 1
     monkeypatch.setenv("EVT_LANES", "1")
     assert _lib.default_lanes("bf16", 256) == 1
     monkeypatch.setenv("EVT_LANES", "3")
