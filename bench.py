@@ -361,7 +361,10 @@ def main():
                        "model": args.model, "global_batch": G, "per_gpu_batch": cap,
                        "seq_len": model.cfg.res(0) ** 2 if swin else model.cfg.tokens,
                        "parallelism": par,
-                       "gemm_variant": args.gemm_variant or "automatic"},
+                       "gemm_variant": args.gemm_variant or "automatic",
+                       # batch lanes of the handle (evt_model_set_lanes); the roofline's per-role
+                       # times come from profiled forwards, which run as one lane
+                       "lanes": model.lanes()},
             "model_roofline": {"achieved_tflops": round(imgs_per_s * gflop_img / world / 1e3, 2),
                                "peak": peak, "frac": round(imgs_per_s * gflop_img / world / 1e3
                                                            / peak, 4),
