@@ -179,6 +179,10 @@ struct evt_model {
   std::vector<char> lane_own;        // lane_s[i] created (and destroyed) by the library
   std::vector<hipEvent_t> lane_ev;   // [0]: fork, [1 + i]: lane i done
   bool is_lane = false;              // a child: weights and lanes belong to the parent
+  // T2T-ViT lanes: their persistent GEMMs keep one block per CU at 2-4 tile rounds (the other
+  // lane fills the CUs a balanced grid leaves idle; measured +2.9 % on T2T-ViT-14 bs256, while
+  // Swin lanes measured -1.3 % without the balancing: DESIGN.md, batch lanes)
+  int no_balance = 0;
 };
 
 namespace {
@@ -428,6 +432,7 @@ GemmParams dense_params(const evt_model* m, const DenseW& w, const DenseCall& c)
       (((uintptr_t)c.C | (uintptr_t)c.resid) & 15) == 0)
     p.vec_ok = 2;
   p.colsum = w.colsum;
+  p.no_balance = m->no_balance;
   p.stats_in = c.stats_in;
   p.rstats = c.rstats;
   p.rgamma = c.rgamma;
@@ -1347,6 +1352,7 @@ int evt_model_set_lanes(evt_model* m, int lanes, void* stream) {
       c->prof_gbytes.clear();
       c->is_lane = true;
       c->max_batch = per;
+      c->no_balance = m->family == 1 ? 1 : 0;
       c->u = c->kqvb = c->pout = c->zrow = c->x = c->xm = c->qkv = c->o = c->hbuf = nullptr;
       c->hh = c->sk = c->pooled = c->apatch = c->qa = c->qh = nullptr;
       c->su = c->tstats = c->part = c->sx = c->sm = c->lnst = nullptr;

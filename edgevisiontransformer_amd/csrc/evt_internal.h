@@ -61,6 +61,8 @@ struct GemmParams {
   int64_t ks_stride;                  // fp32 partial C of split z at C + z * ks_stride
   int xgroups;                        // persistent 256x256 walk: XCD groups that each own
                                       // ntiles / xgroups weight panels (0 / 1: one group)
+  int no_balance;                     // 1: persistent grids of 2-4 tile rounds keep one block per
+                                      // CU (the launching model's lanes fill the idle CUs)
 };
 constexpr int GEMM_BM = 128;
 constexpr int GEMM_BN = 128;

@@ -2572,7 +2572,7 @@ hipError_t launch_pers(const GemmParams& p, hipStream_t s) {
   // not applied there. evt_set_gemm_variant 36: never (the tile -> block assignment only: bitwise
   // the same outputs); EVT_GRID_BALANCE=0 / 2: never / always (A/B)
   const int rounds = (total + G - 1) / G;
-  const int bal = g_gemm_variant == 36 ? 0 : g_grid_balance;
+  const int bal = (g_gemm_variant == 36 || p.no_balance) ? 0 : g_grid_balance;
   if (total > G && G >= 8 && (bal == 2 || (bal == 1 && rounds <= 4)))
     G = min(G, (((total + rounds - 1) / rounds) + 7) & ~7);
   // one round (one block per tile): up to a multiple of 8 blocks (the surplus exits at once) so

@@ -10,7 +10,7 @@
 #   bench:<args>            one bench.py line (e.g. bench:--batch,64,--steps,50)
 #   ab:<args>               alternating A/B of bench.py <args> over the arms in $ARMS, $ROUNDS times;
 #                           an arm is "lib=<path>" (EVT_LIB), "var=<n>" (--gemm-variant) or "base"
-#                           or "env=NAME=VALUE" (an environment switch)
+#                           or "env=NAME=VALUE[+NAME=VALUE...]" (environment switches)
 #                           (PROBE=1: with the per-role probe; ROLES="attention qkv": print those roles)
 #   kstats:<args>           rocprofv3 kernel trace + stats of bench.py <args> -> <name>_kstats.txt
 #   pmc:<name>:<role>:<args>  FETCH_SIZE / WRITE_SIZE passes over real forwards -> pmc_<name>.json
@@ -42,7 +42,7 @@ for STEP in "$@"; do
     for i in $(seq $ROUNDS); do
       for arm in ${ARMS:-base}; do
         n=$(name_of "ab $a $arm $i"); extra=""; envl=""
-        case $arm in lib=*) envl="EVT_LIB=$R/${arm#lib=}";; var=*) extra="--gemm-variant ${arm#var=}";; env=*) envl="${arm#env=}";; esac
+        case $arm in lib=*) envl="EVT_LIB=$R/${arm#lib=}";; var=*) extra="--gemm-variant ${arm#var=}";; env=*) envl="${arm#env=}"; envl=${envl//+/ };; esac
         env $envl timeout -k 10 300 python bench.py $a $extra --cpu-seconds 0 $np > $O/$n.jsonl 2>&1 || { tail -5 $O/$n.jsonl; exit 1; }
         summ $O/$n.jsonl "$arm#$i"
       done
