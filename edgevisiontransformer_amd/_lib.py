@@ -208,7 +208,7 @@ def stream_ptr(device=None) -> int:
 
 # evt_model_set_lanes policy of the mirrors: two lanes from 128 images for T2T-ViT / Swin in bf16
 # and for ViT in fp32. Measured round 6 (bench.py A/B on one box per call, profiles/
-# r06_lanes_ab.txt): T2T-ViT-14 bs256 +0.7-1.8 %, Swin-T bs256 +0.5-3.3 %, DeiT-tiny fp32 bs256
+# r06_lanes_ab.txt): T2T-ViT-14 bs256 +3.1 %, Swin-T bs256 +0.5-3.3 %, DeiT-tiny fp32 bs256
 # +19 %, logits bitwise equal; bf16 ViT stays one lane (DeiT-base bs512 / bs64 slower split).
 LANES_MIN_BATCH = 128
 
