@@ -64,3 +64,12 @@ def test_bench_weak_two_ranks(gpu, tmp_path):
         parts.append(_single(torch.randn((8, 3, 224, 224), generator=g, device="cuda",
                                          dtype=torch.float32)))
     assert np.array_equal(got, np.concatenate(parts))
+
+
+def test_bench_weak_two_ranks_laned(gpu, tmp_path):
+    """The multi-rank path with laned handles (T2T-ViT-14, 128 images per rank: two batch lanes
+    each), both ranks on cuda:0: the line reports the lanes and finite gathered logits."""
+    line, got = _run_two_ranks(tmp_path, ["--model", "t2t_vit_14", "--batch", "128"], 29633)
+    assert line["n_gpus"] == 2 and line["config"]["lanes"] == 2 and line["logits_finite"]
+    assert got.shape == (256, 1000)
+
